@@ -1,0 +1,133 @@
+/*
+ * zfft.h -- C-ABI of the MI355X Zoom-FFT spectrum/waterfall engine (libzfft.so).
+ *
+ * Drop-in boundary for pypanadapter's IQ -> waterfall-line hot path.  The reference has
+ * no FFI: the path is inline numpy/scipy.  Each entry point below replaces a reference
+ * call site (file:line under alfille/pypanadapter):
+ *
+ *   zfft_process        ApplicationDisplay.update (pypanadapter_spectrum.py:2102-2119):
+ *                       zoomfft -> welch -> fftshift/crop -> 20*log10, one row per frame;
+ *                       PSD.update (pypanadapter_thread.py:1513-1548), threaded caller.
+ *   zfft_decimate       ApplicationDisplay.zoomfft (pypanadapter_spectrum.py:2088-2100).
+ *   zfft_waterfall_*    Waterfall.init_image / image_update (pypanadapter_spectrum.py:
+ *                       1625-1664), kept as a device ring + offset instead of np.roll.
+ *   zfft_waterfall_reset ApplicationDisplay.on_invertscroll_clicked (S:2074-2077).
+ *
+ * Conventions: IQ is interleaved float32 (complex64, numpy's layout).  Rows are float32,
+ * length n_win, dB = 20*log10(PSD) exactly as the reference computes it.  Every function
+ * returns 0 on success or a negative ZFFT_E* code; zfft_last_error() (thread-local)
+ * holds the message.  A plan is not re-entrant: one plan per calling thread; plans on
+ * different devices run concurrently.  The caller owns all host buffers; the plan owns
+ * its device buffers, HIP stream and tables.
+ */
+#ifndef ZFFT_H
+#define ZFFT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZFFT_VERSION 1
+
+/* error codes */
+#define ZFFT_OK 0
+#define ZFFT_EINVAL (-1)       /* bad argument / config (ValueError in the Python shim) */
+#define ZFFT_ESHORT (-2)       /* frame too short: a decimation stage has <= 27 samples  */
+#define ZFFT_EHIP (-3)         /* HIP runtime failure                                    */
+#define ZFFT_ENOMEM (-4)       /* device or host allocation failed                       */
+#define ZFFT_ENODEV (-5)       /* no HIP device                                          */
+#define ZFFT_EUNSUPPORTED (-6) /* valid in the reference but not built in this version   */
+
+/* window kinds: scipy.signal.get_window(kind, M) with fftbins=True (periodic), the taper
+ * list of FFTTaperingControl (pypanadapter_spectrum.py:1222-1243) */
+enum zfft_window_kind {
+  ZFFT_WIN_HAMMING = 0, /* AppState.fft_tapering default, S:1492 */
+  ZFFT_WIN_HANN = 1,
+  ZFFT_WIN_BLACKMAN = 2,
+  ZFFT_WIN_BLACKMANHARRIS = 3,
+  ZFFT_WIN_NUTTALL = 4,
+  ZFFT_WIN_FLATTOP = 5,
+  ZFFT_WIN_BARTHANN = 6,
+  ZFFT_WIN_BARTLETT = 7,
+  ZFFT_WIN_TRIANG = 8,
+  ZFFT_WIN_BOHMAN = 9,
+  ZFFT_WIN_PARZEN = 10,
+  ZFFT_WIN_BOXCAR = 11,
+  ZFFT_WIN_KAISER = 12,           /* window_param[0] = beta              */
+  ZFFT_WIN_GAUSSIAN = 13,         /* window_param[0] = std               */
+  ZFFT_WIN_GENERAL_GAUSSIAN = 14, /* window_param = {p, sig}              */
+  ZFFT_WIN_TUKEY = 15,            /* window_param[0] = alpha             */
+  ZFFT_WIN_ARRAY = 100            /* caller-supplied float window (any scipy window) */
+};
+
+typedef struct zfft_config {
+  int32_t n_fft;           /* N: power of two, 32..16384 (AppState.fft_size, S:1397)        */
+  int32_t zoom;            /* power of two, 1..512 (AppState.fft_ratio, S:2079-2086)        */
+  int32_t n_win;           /* W: row length, even, 2..N (N_WIN S:1757; T:1542)              */
+  int32_t window_kind;     /* enum zfft_window_kind                                         */
+  double fs;               /* sample rate, Hz (panadapter.SampleRate)                       */
+  double f_lo;             /* LO frequency, Hz; the reference hard-codes 1.0 (S:2090)       */
+  double window_param[2];  /* see window kinds                                              */
+  int32_t scroll;          /* waterfall direction, +1 or -1 (AppState.scroll, S:1496)       */
+  int32_t in_dtype;        /* 0 = complex64 (interleaved f32); others reserved              */
+  int32_t device;          /* HIP device ordinal                                            */
+  int32_t flip_input;      /* reserved, must be 0 (np.flip of RTL-SDR sources, S:543)       */
+} zfft_config;
+
+typedef struct zfft_plan zfft_plan;
+
+/* Create a plan.  window_or_null: with ZFFT_WIN_ARRAY, a float window of length n_fft (the
+ * array welch receives; frames whose decimated length is < n_fft are then rejected, as
+ * scipy rejects a window longer than the input). */
+int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_plan **out);
+int zfft_plan_destroy(zfft_plan *plan);
+
+/* Host-buffer path: n_frames frames of n_samples IQ each (frame-major), rows_out holds
+ * n_frames*n_win floats.  Synchronous.  PCIe-inclusive. */
+int zfft_process(zfft_plan *plan, const void *iq, int64_t n_samples, int32_t n_frames,
+                 float *rows_out);
+
+/* Device-buffer path: d_iq and d_rows are device pointers on the plan's device.  Enqueued
+ * on `hip_stream` (a hipStream_t; NULL = the plan's own stream); returns without syncing. */
+int zfft_process_device(zfft_plan *plan, const void *d_iq, int64_t n_samples, int32_t n_frames,
+                        float *d_rows, void *hip_stream);
+
+/* zoomfft (S:2088-2100): LO mix then log2(zoom) x decimate(x, 2).  out_iq receives
+ * zfft_decimated_length(n_samples, zoom) complex64 samples.  Synchronous, host buffers. */
+int zfft_decimate(zfft_plan *plan, const void *iq, int64_t n_samples, void *out_iq,
+                  int64_t *out_len);
+int64_t zfft_decimated_length(int64_t n_samples, int32_t zoom);
+
+/* Waterfall ring: H = n_win/4 rows of n_win floats, reference row order on read. */
+int zfft_waterfall_push(zfft_plan *plan, const float *row /* host, n_win; NULL = last row of
+                                                             the last zfft_process* frame */);
+int zfft_waterfall_push_device(zfft_plan *plan, const float *d_rows, int32_t count,
+                               void *hip_stream);
+int zfft_waterfall_read(zfft_plan *plan, float *img_out /* host, H*n_win */);
+int zfft_waterfall_reset(zfft_plan *plan, int32_t scroll);
+int zfft_waterfall_shape(const zfft_plan *plan, int32_t *rows, int32_t *cols);
+
+/* Native window generation (fp64), for tests and for callers without scipy. */
+int zfft_window_values(int32_t kind, const double *param, int32_t length, double *out);
+
+/* Block size / warm-up of the device decimator (0 = automatic).  Diagnostics. */
+int zfft_plan_tune(zfft_plan *plan, int32_t block, int32_t warmup);
+
+/* Per-launch HIP-event timing of zfft_process*: when enabled, the plan brackets every
+ * kernel it launches with events on the launch stream; zfft_plan_timings then returns the
+ * durations (ms) of the last call, in launch order: for each decimation stage k the
+ * forward and backward pass, then the Welch-row kernel.  Diagnostics; adds event records. */
+int zfft_plan_timing(zfft_plan *plan, int32_t enable);
+int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *count);
+
+const char *zfft_last_error(void);
+int zfft_device_count(void);
+int zfft_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZFFT_H */

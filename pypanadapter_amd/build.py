@@ -1,0 +1,43 @@
+"""Build libzfft.so in-tree with hipcc for gfx950 (no JIT cache, so it travels with gpurun)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libzfft.so")
+SOURCES = ["zfft_kernels.hip", "zfft_plan.cpp", "windows.cpp"]
+HEADERS = ["zfft_internal.h", "cheby1_q2.h", os.path.join("..", "..", "include", "zfft.h")]
+ARCH = os.environ.get("ZFFT_OFFLOAD_ARCH", "gfx950")
+
+
+def _newest_input_mtime() -> float:
+    paths = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def needs_build() -> bool:
+    return not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < _newest_input_mtime()
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB_PATH
+    os.makedirs(LIB_DIR, exist_ok=True)
+    hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    cmd += [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

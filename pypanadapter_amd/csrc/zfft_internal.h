@@ -1,0 +1,66 @@
+// Internal declarations shared by the plan (zfft_plan.cpp) and the HIP kernels
+// (zfft_kernels.hip).  Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace zfft {
+
+constexpr int kPad = 27;      // sosfiltfilt odd-extension length (3 * ntaps)
+constexpr int kMaxLdsFft = 16384;
+
+// float32 copy of the ↓2 Chebyshev-I SOS cascade (cheby1_q2.h); passed by value as a
+// kernel argument so every coefficient lives in SGPRs.
+struct Sos32 {
+  float b0, b1, b2;  // section 0 numerator; sections 1..3 are exactly [1, 2, 1]
+  float a1[4], a2[4];
+  float zi[4][2];    // sosfilt_zi
+};
+
+Sos32 sos32();
+
+// --- kernels (zfft_kernels.hip); all enqueue on `st`, return hipError_t of the launch ---
+struct StageGeom {
+  int n;        // stage input length
+  int nblk;     // blocks per frame (each block one thread)
+  int block;    // samples per block (S)
+  int warmup;   // warm-up samples (W)
+};
+
+hipError_t launch_iir_forward(const float2 *in, int64_t in_stride, const float2 *lo, bool mix,
+                              float2 *yf, int64_t yf_stride, const StageGeom &g, int frames,
+                              hipStream_t st);
+hipError_t launch_iir_backward(const float2 *yf, int64_t yf_stride, float2 *out,
+                               int64_t out_stride, const StageGeom &g, int frames,
+                               hipStream_t st);
+
+struct WelchGeom {
+  int n_fft, log2n;
+  int n_win;
+  int nperseg, step, nseg;
+  float scale;  // 1 / (fs * sum(w^2) * nseg)
+};
+
+hipError_t launch_welch_rows(const float2 *x, int64_t x_stride, const float *win,
+                             const float2 *tw, const WelchGeom &g, float *rows,
+                             int64_t row_stride, int frames, hipStream_t st);
+
+hipError_t launch_waterfall_init(float *ring, int H, int W, hipStream_t st);
+hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,
+                                 int64_t row_stride, int count, int64_t off0, int scroll,
+                                 hipStream_t st);
+hipError_t launch_waterfall_read(const float *ring, int H, int W, int64_t off, float *img,
+                                 hipStream_t st);
+hipError_t launch_mix(const float2 *in, const float2 *lo, float2 *out, int64_t n,
+                      hipStream_t st);
+
+// --- host helpers ---
+void set_error(const std::string &msg);
+bool window_kind_native(int kind);
+bool make_window(int kind, const double *param, int M, std::vector<double> &out);
+
+}  // namespace zfft

@@ -1,0 +1,546 @@
+// zfft_plan.cpp -- plan, workspace and C-ABI entry points of libzfft.so.
+//
+// One plan = one (N, zoom, W, window, fs, f_lo, scroll) configuration on one device, the
+// analogue of the AppState fields the reference re-reads every frame
+// (pypanadapter_spectrum.py:1492-1497, 2102-2119).  It owns the HIP stream, the LO /
+// window / twiddle tables, a grow-only workspace and the waterfall ring.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cheby1_q2.h"
+#include "zfft.h"
+#include "zfft_internal.h"
+
+namespace zfft {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+
+Sos32 sos32() {
+  static const Sos32 c = [] {
+    Sos32 s{};
+    s.b0 = (float)kDecimSos[0][0];
+    s.b1 = (float)kDecimSos[0][1];
+    s.b2 = (float)kDecimSos[0][2];
+    for (int k = 0; k < 4; ++k) {
+      s.a1[k] = (float)kDecimSos[k][4];
+      s.a2[k] = (float)kDecimSos[k][5];
+      s.zi[k][0] = (float)kDecimZi[k][0];
+      s.zi[k][1] = (float)kDecimZi[k][1];
+    }
+    return s;
+  }();
+  return c;
+}
+
+namespace {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T *as() const { return static_cast<T *>(p); }
+};
+
+bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
+int ilog2(int64_t v) {
+  int r = 0;
+  while ((int64_t(1) << r) < v) ++r;
+  return r;
+}
+
+int fail(int code, const std::string &msg) {
+  set_error(msg);
+  return code;
+}
+
+int hip_fail(hipError_t e, const char *where) {
+  return fail(ZFFT_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+}  // namespace zfft
+
+using namespace zfft;
+
+struct zfft_plan {
+  zfft_config cfg{};
+  int K = 0;  // log2(zoom) decimation stages
+  hipStream_t stream = nullptr;
+  std::vector<float> user_window;
+  DevBuf lo, win, tw, in, yf, ping, pong, rows, ring, img, one_row, dec;
+  int64_t lo_len = 0;
+  int win_len = -1;
+  double win_ss = 0.0;
+  int block_override = 0, warm_override = 0;
+  int H = 0, W = 0;
+  int64_t off = 0;
+  bool wf_ready = false;
+  const float *last_row = nullptr;  // device row of the last processed frame
+  bool timing = false;
+  std::vector<hipEvent_t> events;    // 2 per launch when timing is on
+  int n_marks = 0;
+};
+
+namespace {
+
+// Timing marks: an event before the first launch and after each launch of a call.
+void mark(zfft_plan *p, hipStream_t st) {
+  if (!p->timing) return;
+  if ((int)p->events.size() <= p->n_marks) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return;
+    p->events.push_back(ev);
+  }
+  (void)hipEventRecord(p->events[p->n_marks++], st);
+}
+
+// Stage lengths: n_0 = L, n_{k+1} = ceil(n_k / 2)  (decimate(...)[::2]).
+std::vector<int64_t> stage_lengths(int64_t L, int K) {
+  std::vector<int64_t> n{L};
+  for (int k = 0; k < K; ++k) n.push_back((n.back() + 1) / 2);
+  return n;
+}
+
+int choose_block(const zfft_plan *p, int64_t e, int frames) {
+  if (p->block_override > 0) return p->block_override;
+  // Enough lanes to fill 256 CUs x 8+ waves; larger blocks amortise the warm-up.
+  int S = 8192;
+  while (S > 512 && (int64_t)frames * ((e + S - 1) / S) < 131072) S >>= 1;
+  return S;
+}
+
+int warmup(const zfft_plan *p) { return p->warm_override > 0 ? p->warm_override : 192; }
+
+int ensure_lo(zfft_plan *p, int64_t L) {
+  if (p->lo_len >= L) return ZFFT_OK;
+  int64_t cap = L;
+  std::vector<float2> h(cap);
+  const double r = p->cfg.f_lo / p->cfg.fs, sq2 = std::sqrt(2.0);
+  for (int64_t n = 0; n < cap; ++n) {
+    // lo[n] = sqrt(2) exp(-2 pi i f_lo n / fs) on integer n (S:2091-2093)
+    const double turns = std::fmod((double)n * r, 1.0);
+    const double ph = -2.0 * M_PI * turns;
+    h[n] = make_float2((float)(sq2 * std::cos(ph)), (float)(sq2 * std::sin(ph)));
+  }
+  hipError_t e = p->lo.ensure(cap * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "LO table allocation failed");
+  e = hipMemcpy(p->lo.p, h.data(), cap * sizeof(float2), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "LO table upload");
+  p->lo_len = cap;
+  return ZFFT_OK;
+}
+
+// welch builds get_window(window, nperseg); nperseg = min(N, L_d) (short-input branch).
+int ensure_window(zfft_plan *p, int nperseg) {
+  if (p->win_len == nperseg) return ZFFT_OK;
+  std::vector<double> w;
+  if (p->cfg.window_kind == ZFFT_WIN_ARRAY) {
+    if (nperseg != p->cfg.n_fft)
+      return fail(ZFFT_EINVAL, "window is longer than input signal (array window of length "
+                               "n_fft, decimated frame shorter than n_fft)");
+    w.assign(p->user_window.begin(), p->user_window.end());
+  } else if (!make_window(p->cfg.window_kind, p->cfg.window_param, nperseg, w)) {
+    return fail(ZFFT_EINVAL, "window generation failed");
+  }
+  std::vector<float> wf(nperseg);
+  double ss = 0.0;
+  for (int i = 0; i < nperseg; ++i) {
+    wf[i] = (float)w[i];
+    ss += w[i] * w[i];
+  }
+  hipError_t e = p->win.ensure(p->cfg.n_fft * sizeof(float));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "window allocation failed");
+  e = hipMemcpy(p->win.p, wf.data(), nperseg * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "window upload");
+  p->win_len = nperseg;
+  p->win_ss = ss;
+  return ZFFT_OK;
+}
+
+int check_lengths(const zfft_plan *p, int64_t L, int32_t frames, std::vector<int64_t> &n) {
+  if (L < 1 || frames < 1) return fail(ZFFT_EINVAL, "n_samples and n_frames must be >= 1");
+  if (L > (int64_t)1 << 30) return fail(ZFFT_EINVAL, "n_samples too large (max 2^30)");
+  n = stage_lengths(L, p->K);
+  for (int k = 0; k < p->K; ++k)
+    if (n[k] <= kPad)
+      return fail(ZFFT_ESHORT, "The length of the input vector x must be greater than padlen, "
+                               "which is 27 (decimation stage " + std::to_string(k) + " has " +
+                               std::to_string(n[k]) + " samples)");
+  return ZFFT_OK;
+}
+
+// Decimation cascade on frames x L (device), result left in *out / *out_stride.
+int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
+                  const std::vector<int64_t> &n, const float2 **out, int64_t *out_stride,
+                  hipStream_t st) {
+  if (p->K == 0) {
+    *out = d_iq;
+    *out_stride = L;
+    return ZFFT_OK;
+  }
+  int rc = ensure_lo(p, L);
+  if (rc) return rc;
+  hipError_t e = p->yf.ensure((size_t)frames * (L + 2 * kPad) * sizeof(float2));
+  if (e == hipSuccess) e = p->ping.ensure((size_t)frames * n[1] * sizeof(float2));
+  if (e == hipSuccess && p->K > 1) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+  const float2 *cur = d_iq;
+  int64_t cur_stride = L;
+  mark(p, st);
+  for (int k = 0; k < p->K; ++k) {
+    const int64_t ek = n[k] + 2 * kPad;
+    StageGeom g;
+    g.n = (int)n[k];
+    g.block = choose_block(p, ek, frames);
+    g.nblk = (int)((ek + g.block - 1) / g.block);
+    g.warmup = warmup(p);
+    e = launch_iir_forward(cur, cur_stride, p->lo.as<float2>(), k == 0, p->yf.as<float2>(), ek, g,
+                           frames, st);
+    if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
+    mark(p, st);
+    float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
+    e = launch_iir_backward(p->yf.as<float2>(), ek, dst, n[k + 1], g, frames, st);
+    if (e != hipSuccess) return hip_fail(e, "iir_backward launch");
+    mark(p, st);
+    cur = dst;
+    cur_stride = n[k + 1];
+  }
+  *out = cur;
+  *out_stride = cur_stride;
+  return ZFFT_OK;
+}
+
+int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, float *d_rows,
+                   hipStream_t st) {
+  std::vector<int64_t> n;
+  int rc = check_lengths(p, L, frames, n);
+  if (rc) return rc;
+  const int64_t Ld = n[p->K];
+  const int N = p->cfg.n_fft;
+  const int nperseg = (int)(Ld < N ? Ld : N);
+  rc = ensure_window(p, nperseg);
+  if (rc) return rc;
+  const float2 *x;
+  int64_t xs;
+  p->n_marks = 0;
+  if (p->K == 0) mark(p, st);
+  rc = run_decimator(p, d_iq, L, frames, n, &x, &xs, st);
+  if (rc) return rc;
+  WelchGeom w;
+  w.n_fft = N;
+  w.log2n = ilog2(N);
+  w.n_win = p->cfg.n_win;
+  w.nperseg = nperseg;
+  w.step = nperseg - nperseg / 2;
+  w.nseg = (int)((Ld - nperseg) / w.step + 1);
+  // density scaling 1/(fs*sum(w^2)) and the segment mean (csd average='mean')
+  w.scale = (float)(1.0 / (p->cfg.fs * p->win_ss * (double)w.nseg));
+  hipError_t e = launch_welch_rows(x, xs, p->win.as<float>(), p->tw.as<float2>(), w, d_rows,
+                                   p->cfg.n_win, frames, st);
+  if (e != hipSuccess) return hip_fail(e, "welch_rows launch");
+  mark(p, st);
+  p->last_row = d_rows + (int64_t)(frames - 1) * p->cfg.n_win;
+  return ZFFT_OK;
+}
+
+int ensure_waterfall(zfft_plan *p) {
+  const int W = p->cfg.n_win;
+  if (p->wf_ready && p->W == W) return ZFFT_OK;
+  if (W < 10 || (p->cfg.scroll > 0 && W / 4 < 15) || (p->cfg.scroll < 0 && W / 4 < 10))
+    return fail(ZFFT_EINVAL, "waterfall needs n_win >= 60 (scroll=+1) or >= 40 (scroll=-1): "
+                             "Waterfall.image_update indexes rows 5..14 / -10..-3 (S:1655-1662)");
+  const int H = W / 4;
+  hipError_t e = p->ring.ensure((size_t)H * W * sizeof(float));
+  if (e == hipSuccess) e = p->img.ensure((size_t)H * W * sizeof(float));
+  if (e == hipSuccess) e = p->one_row.ensure((size_t)W * sizeof(float));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "waterfall allocation failed");
+  e = launch_waterfall_init(p->ring.as<float>(), H, W, p->stream);
+  if (e != hipSuccess) return hip_fail(e, "waterfall init");
+  p->H = H;
+  p->W = W;
+  p->off = 0;
+  p->wf_ready = true;
+  return ZFFT_OK;
+}
+
+hipStream_t pick_stream(zfft_plan *p, void *s) { return s ? (hipStream_t)s : p->stream; }
+
+int enter(zfft_plan *p) {
+  if (!p) return fail(ZFFT_EINVAL, "null plan");
+  hipError_t e = hipSetDevice(p->cfg.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  return ZFFT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *zfft_last_error(void) { return g_err.c_str(); }
+int zfft_version(void) { return ZFFT_VERSION; }
+
+int zfft_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int64_t zfft_decimated_length(int64_t n_samples, int32_t zoom) {
+  if (n_samples < 0 || !is_pow2(zoom)) return -1;
+  for (int z = zoom; z > 1; z >>= 1) n_samples = (n_samples + 1) / 2;
+  return n_samples;
+}
+
+int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_plan **out) {
+  if (!cfg || !out) return fail(ZFFT_EINVAL, "null config or output pointer");
+  *out = nullptr;
+  const zfft_config &c = *cfg;
+  if (!is_pow2(c.n_fft) || c.n_fft < 32 || c.n_fft > 65536)
+    return fail(ZFFT_EINVAL, "n_fft must be a power of two in [32, 65536]");
+  if (c.n_fft > kMaxLdsFft)
+    return fail(ZFFT_EUNSUPPORTED, "n_fft > 16384 needs the four-step FFT (not built yet)");
+  if (!is_pow2(c.zoom) || c.zoom > 512) return fail(ZFFT_EINVAL, "zoom must be 1, 2, 4, ..., 512");
+  if (c.n_win < 2 || c.n_win > c.n_fft || (c.n_win & 1))
+    return fail(ZFFT_EINVAL, "n_win must be even and in [2, n_fft]");
+  if (!(c.fs > 0) || !std::isfinite(c.fs) || !std::isfinite(c.f_lo))
+    return fail(ZFFT_EINVAL, "fs must be positive and finite, f_lo finite");
+  if (c.scroll != 1 && c.scroll != -1) return fail(ZFFT_EINVAL, "scroll must be +1 or -1");
+  if (c.in_dtype != 0) return fail(ZFFT_EUNSUPPORTED, "only complex64 input (in_dtype 0)");
+  if (c.flip_input != 0) return fail(ZFFT_EUNSUPPORTED, "flip_input is not built yet");
+  if (c.window_kind == ZFFT_WIN_ARRAY) {
+    if (!window_or_null) return fail(ZFFT_EINVAL, "ZFFT_WIN_ARRAY needs a window array");
+  } else if (!window_kind_native(c.window_kind)) {
+    return fail(ZFFT_EINVAL, "unknown window kind");
+  }
+  int ndev = zfft_device_count();
+  if (ndev < 1) return fail(ZFFT_ENODEV, "no HIP device");
+  if (c.device < 0 || c.device >= ndev) return fail(ZFFT_ENODEV, "device ordinal out of range");
+  hipError_t e = hipSetDevice(c.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+
+  zfft_plan *p = new zfft_plan();
+  p->cfg = c;
+  p->K = ilog2(c.zoom);
+  if (c.window_kind == ZFFT_WIN_ARRAY)
+    p->user_window.assign(window_or_null, window_or_null + c.n_fft);
+  e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "hipStreamCreate");
+  }
+  // FFT twiddles tw[m] = exp(-2 pi i m / N), computed in fp64
+  std::vector<float2> tw(c.n_fft);
+  for (int m = 0; m < c.n_fft; ++m) {
+    const double a = -2.0 * M_PI * (double)m / (double)c.n_fft;
+    tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  e = p->tw.ensure(c.n_fft * sizeof(float2));
+  if (e == hipSuccess)
+    e = hipMemcpy(p->tw.p, tw.data(), c.n_fft * sizeof(float2), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    zfft_plan_destroy(p);
+    return hip_fail(e, "twiddle upload");
+  }
+  *out = p;
+  return ZFFT_OK;
+}
+
+int zfft_plan_destroy(zfft_plan *p) {
+  if (!p) return ZFFT_OK;
+  (void)hipSetDevice(p->cfg.device);
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
+  for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->yf, &p->ping, &p->pong, &p->rows,
+                    &p->ring, &p->img, &p->one_row, &p->dec})
+    b->release();
+  for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+  return ZFFT_OK;
+}
+
+int zfft_plan_tune(zfft_plan *p, int32_t block, int32_t warm) {
+  if (!p || block < 0 || warm < 0) return fail(ZFFT_EINVAL, "bad tune arguments");
+  if (block && (block < 64 || block > (1 << 20)))
+    return fail(ZFFT_EINVAL, "block must be in [64, 2^20]");
+  p->block_override = block;
+  p->warm_override = warm;
+  return ZFFT_OK;
+}
+
+int zfft_plan_timing(zfft_plan *p, int32_t enable) {
+  if (!p) return fail(ZFFT_EINVAL, "null plan");
+  p->timing = enable != 0;
+  p->n_marks = 0;
+  return ZFFT_OK;
+}
+
+int zfft_plan_timings(zfft_plan *p, float *ms_out, int32_t max, int32_t *count) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!ms_out || !count) return fail(ZFFT_EINVAL, "null output");
+  const int n = p->n_marks > 0 ? p->n_marks - 1 : 0;
+  if (n > 0) {
+    hipError_t e = hipEventSynchronize(p->events[n]);
+    if (e != hipSuccess) return hip_fail(e, "event sync");
+  }
+  int k = 0;
+  for (; k < n && k < max; ++k) {
+    float ms = 0.f;
+    hipError_t e = hipEventElapsedTime(&ms, p->events[k], p->events[k + 1]);
+    if (e != hipSuccess) return hip_fail(e, "event elapsed");
+    ms_out[k] = ms;
+  }
+  *count = k;
+  return ZFFT_OK;
+}
+
+int zfft_process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, float *d_rows,
+                        void *hip_stream) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!d_iq || !d_rows) return fail(ZFFT_EINVAL, "null device pointer");
+  return process_device(p, (const float2 *)d_iq, L, frames, d_rows, pick_stream(p, hip_stream));
+}
+
+int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float *rows_out) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!iq || !rows_out) return fail(ZFFT_EINVAL, "null host pointer");
+  if (L < 1 || frames < 1) return fail(ZFFT_EINVAL, "n_samples and n_frames must be >= 1");
+  const size_t in_bytes = (size_t)frames * L * sizeof(float2);
+  const size_t row_bytes = (size_t)frames * p->cfg.n_win * sizeof(float);
+  hipError_t e = p->in.ensure(in_bytes);
+  if (e == hipSuccess) e = p->rows.ensure(row_bytes);
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "staging allocation failed");
+  e = hipMemcpyAsync(p->in.p, iq, in_bytes, hipMemcpyHostToDevice, p->stream);
+  if (e != hipSuccess) return hip_fail(e, "H2D copy");
+  rc = process_device(p, p->in.as<float2>(), L, frames, p->rows.as<float>(), p->stream);
+  if (rc) return rc;
+  e = hipMemcpyAsync(rows_out, p->rows.p, row_bytes, hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+  if (e != hipSuccess) return hip_fail(e, "D2H copy / sync");
+  return ZFFT_OK;
+}
+
+int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t *out_len) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!iq || !out_iq) return fail(ZFFT_EINVAL, "null host pointer");
+  std::vector<int64_t> n;
+  rc = check_lengths(p, L, 1, n);
+  if (rc) return rc;
+  hipError_t e = p->in.ensure((size_t)L * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "staging allocation failed");
+  e = hipMemcpyAsync(p->in.p, iq, (size_t)L * sizeof(float2), hipMemcpyHostToDevice, p->stream);
+  if (e != hipSuccess) return hip_fail(e, "H2D copy");
+  const float2 *x;
+  int64_t xs;
+  if (p->K == 0) {  // zoomfft(x, 1) still mixes (S:2093-2094)
+    rc = ensure_lo(p, L);
+    if (rc) return rc;
+    e = p->dec.ensure((size_t)L * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "allocation failed");
+    e = launch_mix(p->in.as<float2>(), p->lo.as<float2>(), p->dec.as<float2>(), L, p->stream);
+    if (e != hipSuccess) return hip_fail(e, "mix launch");
+    x = p->dec.as<float2>();
+  } else {
+    rc = run_decimator(p, p->in.as<float2>(), L, 1, n, &x, &xs, p->stream);
+    if (rc) return rc;
+  }
+  const int64_t m = n[p->K];
+  e = hipMemcpyAsync(out_iq, x, (size_t)m * sizeof(float2), hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+  if (e != hipSuccess) return hip_fail(e, "D2H copy / sync");
+  if (out_len) *out_len = m;
+  return ZFFT_OK;
+}
+
+int zfft_waterfall_shape(const zfft_plan *p, int32_t *rows, int32_t *cols) {
+  if (!p || !rows || !cols) return fail(ZFFT_EINVAL, "null argument");
+  *rows = p->cfg.n_win / 4;
+  *cols = p->cfg.n_win;
+  return ZFFT_OK;
+}
+
+int zfft_waterfall_reset(zfft_plan *p, int32_t scroll) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (scroll != 1 && scroll != -1) return fail(ZFFT_EINVAL, "scroll must be +1 or -1");
+  p->cfg.scroll = scroll;
+  p->wf_ready = false;  // init_image on the next push / read (S:2074-2077)
+  return ensure_waterfall(p);
+}
+
+int zfft_waterfall_push_device(zfft_plan *p, const float *d_rows, int32_t count,
+                               void *hip_stream) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!d_rows || count < 1) return fail(ZFFT_EINVAL, "bad rows / count");
+  rc = ensure_waterfall(p);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(p, hip_stream);
+  if (st != p->stream) {  // ring init was enqueued on the plan stream
+    hipError_t e = hipStreamSynchronize(p->stream);
+    if (e != hipSuccess) return hip_fail(e, "sync");
+  }
+  hipError_t e = launch_waterfall_push(p->ring.as<float>(), p->H, p->W, d_rows, p->W, count,
+                                       p->off, p->cfg.scroll, st);
+  if (e != hipSuccess) return hip_fail(e, "waterfall push");
+  p->off = ((p->off + (int64_t)count * p->cfg.scroll) % p->H + p->H) % p->H;
+  return ZFFT_OK;
+}
+
+int zfft_waterfall_push(zfft_plan *p, const float *row) {
+  int rc = enter(p);
+  if (rc) return rc;
+  rc = ensure_waterfall(p);
+  if (rc) return rc;
+  const float *src = p->last_row;
+  if (row) {
+    hipError_t e = hipMemcpyAsync(p->one_row.p, row, (size_t)p->W * sizeof(float),
+                                  hipMemcpyHostToDevice, p->stream);
+    if (e != hipSuccess) return hip_fail(e, "H2D row");
+    src = p->one_row.as<float>();
+  }
+  if (!src) return fail(ZFFT_EINVAL, "no row given and no frame processed yet");
+  rc = zfft_waterfall_push_device(p, src, 1, p->stream);
+  if (rc) return rc;
+  hipError_t e = hipStreamSynchronize(p->stream);
+  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "sync");
+}
+
+int zfft_waterfall_read(zfft_plan *p, float *img_out) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!img_out) return fail(ZFFT_EINVAL, "null output");
+  rc = ensure_waterfall(p);
+  if (rc) return rc;
+  hipError_t e = launch_waterfall_read(p->ring.as<float>(), p->H, p->W, p->off, p->img.as<float>(),
+                                       p->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(img_out, p->img.p, (size_t)p->H * p->W * sizeof(float),
+                       hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "waterfall read");
+}
+
+}  // extern "C"

@@ -1,0 +1,184 @@
+"""Host-side engine: one `ZoomFFT` plan per (N, zoom, W, window, fs, f_lo, scroll).
+
+Mirrors the reference's per-frame DSP (pypanadapter_spectrum.py:2088-2119) and its
+waterfall model (S:1625-1664) behind libzfft.so.  Host numpy buffers go through the
+synchronous C-ABI calls; device tensors (torch, on the plan's device) go through
+`process_device`, which enqueues on a caller-supplied HIP stream and does not sync.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, zfft_config
+
+
+def _window_spec(window):
+    """AppState.fft_tapering value -> (kind, params, array_or_None).
+
+    Accepts what the reference stores (S:1358-1363): a scipy window name, a
+    (name, p0[, p1]) tuple, or an explicit array (any scipy window, e.g. chebwin/dpss).
+    """
+    if isinstance(window, np.ndarray) or (isinstance(window, (list,)) and window and
+                                          not isinstance(window[0], str)):
+        return _lib.WIN_ARRAY, (0.0, 0.0), np.ascontiguousarray(window, dtype=np.float32)
+    name, params = (window, ()) if isinstance(window, str) else (window[0], tuple(window[1:]))
+    name = _lib.WINDOW_ALIASES.get(name.lower(), name.lower())
+    if name not in _lib.WINDOW_KINDS:
+        raise ValueError(f"window {window!r} has no native generator; pass it as an array "
+                         "(e.g. scipy.signal.get_window(window, n_fft))")
+    p = [float(v) for v in params] + [0.0, 0.0]
+    return _lib.WINDOW_KINDS[name], (p[0], p[1]), None
+
+
+class ZoomFFT:
+    """A plan: IQ frames -> dB rows (+ the on-device waterfall ring)."""
+
+    def __init__(self, n_fft: int, zoom: int, fs: float, n_win: int | None = None,
+                 window="hamming", f_lo: float = 1.0, scroll: int = 1, device: int = 0):
+        self.lib = _lib.load()
+        self.n_fft, self.zoom, self.fs, self.f_lo = int(n_fft), int(zoom), float(fs), float(f_lo)
+        self.n_win = int(n_win) if n_win is not None else self.n_fft // self.zoom
+        kind, params, arr = _window_spec(window)
+        cfg = zfft_config()
+        cfg.n_fft, cfg.zoom, cfg.n_win, cfg.window_kind = self.n_fft, self.zoom, self.n_win, kind
+        cfg.fs, cfg.f_lo = self.fs, self.f_lo
+        cfg.window_param[0], cfg.window_param[1] = params
+        cfg.scroll, cfg.in_dtype, cfg.device, cfg.flip_input = int(scroll), 0, int(device), 0
+        if arr is not None and arr.size != self.n_fft:
+            raise ValueError("array window must have length n_fft (welch nperseg)")
+        self._window_array = arr  # kept alive for the call
+        self._plan = ctypes.c_void_p()
+        check(self.lib.zfft_plan_create(ctypes.byref(cfg),
+                                        arr.ctypes.data_as(ctypes.c_void_p) if arr is not None else None,
+                                        ctypes.byref(self._plan)), "zfft_plan_create")
+        self.scroll = int(scroll)
+        self.device = int(device)
+
+    # ---------------------------------------------------------------- lifetime
+    def close(self):
+        if getattr(self, "_plan", None) and self._plan.value:
+            self.lib.zfft_plan_destroy(self._plan)
+            self._plan = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def tune(self, block: int = 0, warmup: int = 0):
+        check(self.lib.zfft_plan_tune(self._plan, int(block), int(warmup)), "zfft_plan_tune")
+
+    def set_timing(self, enable: bool) -> None:
+        check(self.lib.zfft_plan_timing(self._plan, int(bool(enable))), "zfft_plan_timing")
+
+    def timings(self) -> list:
+        """Per-launch ms of the last process call (needs set_timing(True)); launch order:
+        [fwd_0, bwd_0, fwd_1, bwd_1, ..., welch]."""
+        buf = (ctypes.c_float * 64)()
+        n = ctypes.c_int32()
+        check(self.lib.zfft_plan_timings(self._plan, buf, 64, ctypes.byref(n)), "zfft_plan_timings")
+        return [float(buf[i]) for i in range(n.value)]
+
+    def launch_names(self) -> list:
+        k = self.zoom.bit_length() - 1
+        names = []
+        for s in range(k):
+            names += [f"iir_forward_s{s}", f"iir_backward_s{s}"]
+        return names + ["welch_rows"]
+
+    # ---------------------------------------------------------------- DSP
+    @staticmethod
+    def _as_iq(x) -> np.ndarray:
+        x = np.asarray(x)
+        if x.dtype != np.complex64:
+            x = x.astype(np.complex64)
+        return np.ascontiguousarray(x)
+
+    def rows(self, frames) -> np.ndarray:
+        """(F, L) or (L,) complex IQ -> (F, W) or (W,) float32 dB rows."""
+        x = self._as_iq(frames)
+        single = x.ndim == 1
+        x2 = x.reshape(1, -1) if single else x
+        F, L = x2.shape
+        out = np.empty((F, self.n_win), dtype=np.float32)
+        check(self.lib.zfft_process(self._plan, x2.ctypes.data_as(ctypes.c_void_p), L, F,
+                                    out.ctypes.data_as(ctypes.c_void_p)), "zfft_process")
+        return out[0] if single else out
+
+    def process_device(self, d_iq_ptr: int, n_samples: int, n_frames: int, d_rows_ptr: int,
+                       stream: int = 0) -> None:
+        """Device pointers (e.g. torch .data_ptr()); enqueued on `stream`, no sync."""
+        check(self.lib.zfft_process_device(self._plan, ctypes.c_void_p(d_iq_ptr), int(n_samples),
+                                           int(n_frames), ctypes.c_void_p(d_rows_ptr),
+                                           ctypes.c_void_p(stream or None)), "zfft_process_device")
+
+    def decimate(self, x) -> np.ndarray:
+        """zoomfft(x, zoom) of the reference (S:2088-2100) -> complex64."""
+        x = self._as_iq(x).ravel()
+        m = self.lib.zfft_decimated_length(len(x), self.zoom)
+        out = np.empty(max(m, 1), dtype=np.complex64)
+        n_out = ctypes.c_int64()
+        check(self.lib.zfft_decimate(self._plan, x.ctypes.data_as(ctypes.c_void_p), len(x),
+                                     out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n_out)),
+              "zfft_decimate")
+        return out[:n_out.value]
+
+    # ---------------------------------------------------------------- waterfall
+    def waterfall_push(self, row=None) -> None:
+        if row is None:
+            check(self.lib.zfft_waterfall_push(self._plan, None), "zfft_waterfall_push")
+            return
+        r = np.ascontiguousarray(row, dtype=np.float32)
+        if r.size != self.n_win:
+            raise ValueError("row length must equal n_win")
+        check(self.lib.zfft_waterfall_push(self._plan, r.ctypes.data_as(ctypes.c_void_p)),
+              "zfft_waterfall_push")
+
+    def waterfall_push_device(self, d_rows_ptr: int, count: int, stream: int = 0) -> None:
+        check(self.lib.zfft_waterfall_push_device(self._plan, ctypes.c_void_p(d_rows_ptr),
+                                                  int(count), ctypes.c_void_p(stream or None)),
+              "zfft_waterfall_push_device")
+
+    def waterfall_shape(self):
+        h, w = ctypes.c_int32(), ctypes.c_int32()
+        check(self.lib.zfft_waterfall_shape(self._plan, ctypes.byref(h), ctypes.byref(w)),
+              "zfft_waterfall_shape")
+        return h.value, w.value
+
+    def waterfall_image(self) -> np.ndarray:
+        h, w = self.waterfall_shape()
+        img = np.empty((h, w), dtype=np.float32)
+        check(self.lib.zfft_waterfall_read(self._plan, img.ctypes.data_as(ctypes.c_void_p)),
+              "zfft_waterfall_read")
+        return img
+
+    def waterfall_reset(self, scroll: int) -> None:
+        check(self.lib.zfft_waterfall_reset(self._plan, int(scroll)), "zfft_waterfall_reset")
+        self.scroll = int(scroll)
+
+
+def native_window(window, length: int) -> np.ndarray:
+    """fp64 window from the library's native generator (no scipy needed)."""
+    lib = _lib.load()
+    kind, params, arr = _window_spec(window)
+    if arr is not None:
+        raise ValueError("array windows are not generated")
+    out = np.empty(length, dtype=np.float64)
+    p = (ctypes.c_double * 2)(*params)
+    check(lib.zfft_window_values(kind, p, int(length), out.ctypes.data_as(ctypes.c_void_p)),
+          "zfft_window_values")
+    return out
+
+
+def device_count() -> int:
+    return int(_lib.load().zfft_device_count())

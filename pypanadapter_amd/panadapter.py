@@ -1,0 +1,136 @@
+"""Drop-in facade for the reference's DSP call sites.
+
+The reference computes each waterfall line inline (pypanadapter_spectrum.py:2102-2119):
+
+    if AppState.fft_ratio > 1:
+        chunk = self.zoomfft(chunk, AppState.fft_ratio)
+    sample_freq, spec = scipy.signal.welch(chunk, fs, window=AppState.fft_tapering,
+                                           nperseg=AppState.fft_size, nfft=AppState.fft_size)
+    spec = np.fft.fftshift(spec)[N//2 - self.N_WIN//2 : N//2 + self.N_WIN//2]
+    psd = 20 * np.log10(abs(spec))
+    self.waterfall.image_update(psd)
+
+With this module those lines become `psd = psd_row(chunk, ...)` and `Waterfall` keeps its
+`image_update(psd)` / `img_array` surface, backed by the device ring.  Like the
+reference, `AppState` fields may change between frames: `PlanCache` re-creates the plan
+whenever (N, zoom, W, window, fs, f_lo) change (S:1753-1757, 2079-2086, 1358-1363).
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+
+from .engine import ZoomFFT
+
+_tls = threading.local()  # a plan is not re-entrant: one cache per calling thread
+
+
+def _key(window):
+    if isinstance(window, np.ndarray):
+        return ("array", window.tobytes())
+    return window if isinstance(window, str) else tuple(window)
+
+
+class PlanCache:
+    """Plan keyed on the AppState fields the reference re-reads every frame."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._key = None
+        self.plan: ZoomFFT | None = None
+
+    def get(self, fs, n_fft, zoom, n_win, window="hamming", f_lo=1.0) -> ZoomFFT:
+        key = (float(fs), int(n_fft), int(zoom), int(n_win), _key(window), float(f_lo))
+        if key != self._key:
+            if self.plan is not None:
+                self.plan.close()
+            self.plan = ZoomFFT(n_fft, zoom, fs, n_win=n_win, window=window, f_lo=f_lo,
+                                device=self.device)
+            self._key = key
+        return self.plan
+
+
+def _cache(device: int) -> PlanCache:
+    caches = getattr(_tls, "caches", None)
+    if caches is None:
+        caches = _tls.caches = {}
+    if device not in caches:
+        caches[device] = PlanCache(device)
+    return caches[device]
+
+
+def zoomfft(x, ratio: int, fs: float, f_lo: float = 1.0, device: int = 0) -> np.ndarray:
+    """ApplicationDisplay.zoomfft (S:2088-2100): LO mix + log2(ratio) x decimate(x, 2)."""
+    plan = _cache(device).get(fs, 32, int(ratio), 2, "hamming", f_lo)
+    return plan.decimate(x)
+
+
+def psd_row(chunk, fs: float, fft_size: int, fft_ratio: int, n_win: int | None = None,
+            window="hamming", f_lo: float = 1.0, device: int = 0) -> np.ndarray:
+    """The row ApplicationDisplay.update hands to waterfall.image_update (S:2102-2119).
+
+    Returns a fresh, writable float64 array (the reference's dtype), length n_win
+    (default N / zoom, i.e. N_WIN after fft_change, S:1757).
+    """
+    n_win = int(fft_size) // int(fft_ratio) if n_win is None else int(n_win)
+    plan = _cache(device).get(fs, fft_size, fft_ratio, n_win, window, f_lo)
+    return plan.rows(chunk).astype(np.float64)
+
+
+def thread_psd_row(chunk, fs: float, fft_size: int, fft_ratio: int, window="hamming",
+                   f_lo: float = 1.0, device: int = 0):
+    """PSD.update of the threaded variant (pypanadapter_thread.py:1513-1548): skips chunks
+    shorter than fft_size (T:1522-1523) and crops W = 2*int(0.5*N/zoom) (T:1542)."""
+    if len(chunk) < fft_size:
+        return None
+    n_win = 2 * int(0.5 * fft_size / fft_ratio)
+    return psd_row(chunk, fs, fft_size, fft_ratio, n_win, window, f_lo, device)
+
+
+class Waterfall:
+    """Waterfall.init_image / image_update / img_array (S:1625-1664) on the device ring.
+
+    `image_update(psd)` stamps the grid into the caller's row in place (as S:1646-1648
+    does; the reference then plots that same stamped row, S:2130), writes it as the new
+    line, rolls by `scroll` and stamps the tick marks.  `img_array` materialises the
+    image in the reference's row order (float64, like the reference's array).
+    """
+
+    def __init__(self, scroll: int = 1, device: int = 0, fs: float = 2.4e6):
+        self.scroll = int(scroll)
+        self.device = device
+        self.fs = fs
+        self.fftwidth = 0
+        self._plan: ZoomFFT | None = None
+
+    def _ensure(self, width: int):
+        if width != self.fftwidth or self._plan is None:
+            if self._plan is not None:
+                self._plan.close()
+            n_fft = 1 << max(5, (width - 1).bit_length())
+            self._plan = ZoomFFT(n_fft, 1, self.fs, n_win=width, scroll=self.scroll,
+                                 device=self.device)
+            self.fftwidth = width
+
+    def init_image(self):
+        if self._plan is not None:
+            self._plan.waterfall_reset(self.scroll)
+
+    def set_scroll(self, scroll: int):
+        """ApplicationDisplay.on_invertscroll_clicked (S:2074-2077): new direction + init."""
+        self.scroll = int(scroll)
+        self.init_image()
+
+    def image_update(self, psd: np.ndarray) -> None:
+        width = int(np.size(psd))
+        self._ensure(width)
+        for x in (0, width // 2, width - 1):
+            psd[x] = 0
+        self._plan.waterfall_push(np.asarray(psd, dtype=np.float32))
+
+    @property
+    def img_array(self) -> np.ndarray:
+        if self._plan is None:
+            raise AttributeError("img_array is created by the first image_update")
+        return self._plan.waterfall_image().astype(np.float64)
