@@ -164,10 +164,12 @@ def main():
     plan = ZoomFFT(N, zoom, fs, n_win=W, device=local)
     if args.block or args.warm:
         plan.tune(args.block, args.warm)
+    stream = torch.cuda.Stream(dev)  # a real stream: the null stream's handle (0) would be
+    torch.cuda.set_stream(stream)    # read by the C-ABI as "the plan's own stream"
+    sp = stream.cuda_stream
     x = make_frames(torch, F, L, cfg, dev, 1234 + rank)
     rows = torch.empty((F, W), dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    torch.cuda.synchronize(dev)
 
     def step():
         plan.process_device(x.data_ptr(), L, F, rows.data_ptr(), sp)

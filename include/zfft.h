@@ -90,7 +90,7 @@ int zfft_process(zfft_plan *plan, const void *iq, int64_t n_samples, int32_t n_f
                  float *rows_out);
 
 /* Device-buffer path: d_iq and d_rows are device pointers on the plan's device.  Enqueued
- * on `hip_stream` (a hipStream_t; NULL = the plan's own stream); returns without syncing. */
+ * on `hip_stream` (a hipStream_t; NULL = HIP's default stream); returns without syncing. */
 int zfft_process_device(zfft_plan *plan, const void *d_iq, int64_t n_samples, int32_t n_frames,
                         float *d_rows, void *hip_stream);
 

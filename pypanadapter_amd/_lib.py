@@ -7,6 +7,7 @@ There is no CPU fallback: if the library is missing the import of the engine fai
 from __future__ import annotations
 
 import ctypes
+import importlib.util
 import os
 
 from .build import LIB_PATH
@@ -63,11 +64,31 @@ class ZfftError(RuntimeError):
     pass
 
 
+def _share_hip_runtime_with_torch() -> None:
+    """PyTorch-ROCm ships its own libamdhip64.so (file name without the .7 suffix but the
+    same SONAME, libamdhip64.so.7).  If libzfft.so loads first, the dynamic linker maps
+    /opt/rocm's runtime under that SONAME and torch later maps its own file too: two HIP
+    runtimes in one process, and torch then reports "No HIP GPUs are available".  When
+    torch is installed, pre-load its runtime globally so libzfft.so binds to that one."""
+    if os.environ.get("ZFFT_HIP_RUNTIME", "") == "system":
+        return
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if not spec or not spec.submodule_search_locations:
+        return
+    hip = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+
+
 def load(path: str = LIB_PATH):
     """Load libzfft.so; raises OSError (loudly) when it has not been built."""
     global _lib
     if _lib is not None:
         return _lib
+    _share_hip_runtime_with_torch()
     if not os.path.exists(path):
         raise OSError(f"libzfft.so not built at {path}: run `python -m pypanadapter_amd.build` "
                       "(there is no CPU fallback)")

@@ -24,18 +24,24 @@ struct Sos32 {
 Sos32 sos32();
 
 // --- kernels (zfft_kernels.hip); all enqueue on `st`, return hipError_t of the launch ---
+// Intermediates use the frame-group-interleaved (FGI) layout: element (f, j) of a
+// per-frame sequence of length len lives at ((f/64)*len + j)*64 + f%64 (float2 units);
+// buffers hold ngroups = ceil(frames/64) full groups.
 struct StageGeom {
   int n;        // stage input length
-  int nblk;     // blocks per frame (each block one thread)
-  int block;    // samples per block (S)
-  int warmup;   // warm-up samples (W)
+  int nblk;     // blocks per frame: ceil((n + 27) / block)
+  int block;    // S, samples per block (multiple of 16)
+  int warmup;   // W, warm-up samples (multiple of 16)
+  int ngroups;  // 64-frame groups
 };
 
-hipError_t launch_iir_forward(const float2 *in, int64_t in_stride, const float2 *lo, bool mix,
-                              float2 *yf, int64_t yf_stride, const StageGeom &g, int frames,
-                              hipStream_t st);
-hipError_t launch_iir_backward(const float2 *yf, int64_t yf_stride, float2 *out,
-                               int64_t out_stride, const StageGeom &g, int frames,
+hipError_t launch_iir_forward_mix(const float2 *in, int64_t L, int frames, const float2 *lo,
+                                  float2 *yf, const StageGeom &g, hipStream_t st);
+hipError_t launch_iir_forward_fgi(const float2 *in, float2 *yf, const StageGeom &g,
+                                  hipStream_t st);
+hipError_t launch_iir_backward(const float2 *yf, float2 *out, const StageGeom &g,
+                               hipStream_t st);
+hipError_t launch_deinterleave(const float2 *in, int64_t len, int frames, float2 *out,
                                hipStream_t st);
 
 struct WelchGeom {
@@ -45,9 +51,9 @@ struct WelchGeom {
   float scale;  // 1 / (fs * sum(w^2) * nseg)
 };
 
-hipError_t launch_welch_rows(const float2 *x, int64_t x_stride, const float *win,
-                             const float2 *tw, const WelchGeom &g, float *rows,
-                             int64_t row_stride, int frames, hipStream_t st);
+hipError_t launch_welch_rows(const float2 *x, bool fgi_layout, int64_t len, const float *win,
+                             const float2 *tw, const WelchGeom &g, float *rows, int frames,
+                             hipStream_t st);
 
 hipError_t launch_waterfall_init(float *ring, int H, int W, hipStream_t st);
 hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,

@@ -65,110 +65,252 @@ __device__ __forceinline__ v2f cascade(v2f u, IirState &s, const Sos32 &c) {
   return u;
 }
 
-// ------------------------------------------------------------------ forward pass
-// yf[j], j in [0, n+54): sosfilt over the odd-extended stage input, state zi*ext[0].
-template <bool MIX>
-__global__ __launch_bounds__(256) void iir_forward_kernel(const v2f *__restrict__ in,
-                                                          int64_t in_stride,
-                                                          const v2f *__restrict__ lo,
-                                                          v2f *__restrict__ yf, int64_t yf_stride,
-                                                          StageGeom g, int frames, Sos32 c) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)frames * g.nblk) return;
-  const int f = (int)(gid / g.nblk);
-  const int b = (int)(gid - (int64_t)f * g.nblk);
+// ------------------------------------------------------------------ work mapping
+// Lanes <-> frames: a wave owns one block of one 64-frame group, so every lane runs the
+// same (wave-uniform) sample index j and all loads/stores of an interleaved buffer are
+// one contiguous 512 B row.  Frame-group-interleaved ("FGI") layout of a per-frame
+// sequence of length len: element (f, j) at ((f / 64) * len + j) * 64 + f % 64.
+// Block partition (per stage, in padded "ext" coordinates j in [0, e), e = n + 54):
+//   block 0 = [0, 27 + S), block b >= 1 = [27 + b S, 27 + (b+1) S), last ends at e.
+struct WaveCtx {
+  int lane, b, fg, j0, j1;
+  bool valid;
+};
+
+__device__ __forceinline__ WaveCtx wave_ctx(const StageGeom &g) {
+  WaveCtx w;
+  w.lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  w.valid = wid < g.ngroups * g.nblk;
+  w.b = wid % g.nblk;
+  w.fg = wid / g.nblk;
+  const int e = g.n + 2 * kPad;
+  w.j0 = w.b == 0 ? 0 : kPad + w.b * g.block;
+  w.j1 = min(kPad + (w.b + 1) * g.block, e);
+  return w;
+}
+
+__device__ __forceinline__ int64_t fgi(int fg, int64_t len, int64_t j) {
+  return ((int64_t)fg * len + j) << 6;
+}
+
+constexpr int kU = 8;  // samples per prefetch group (register double buffer)
+
+// Run the cascade over j in [ja, jb) reading src(j) (interleaved row pointer p, stride 64),
+// with a two-group register pipeline: the loads of group g+1 are in flight while group g
+// is computed.  emit(j, y) is called for every step when STORE.
+template <bool STORE, class Src, class Emit>
+__device__ __forceinline__ void pipelined_run(int ja, int jb, Src src, IirState &s,
+                                              const Sos32 &c, Emit emit) {
+  const int cnt = jb - ja;
+  const int full = cnt > 0 ? cnt / kU : 0;
+  int j = ja;
+  if (full > 0) {
+    v2f A[kU], B[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) A[u] = src(j + u);
+    int gi = 0;
+    while (true) {
+      if (gi + 1 < full) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) B[u] = src(j + kU + u);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const v2f o = cascade(A[u], s, c);
+        if constexpr (STORE) emit(j + u, o);
+      }
+      j += kU;
+      if (++gi >= full) break;
+      if (gi + 1 < full) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) A[u] = src(j + kU + u);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const v2f o = cascade(B[u], s, c);
+        if constexpr (STORE) emit(j + u, o);
+      }
+      j += kU;
+      if (++gi >= full) break;
+    }
+  }
+  for (; j < jb; ++j) {
+    const v2f o = cascade(src(j), s, c);
+    if constexpr (STORE) emit(j, o);
+  }
+}
+
+// ------------------------------------------------------------------ forward pass, stage >= 1
+// yf(j) = sosfilt over ext(j), ext = odd extension of the FGI stage input, state zi*ext[0].
+__global__ __launch_bounds__(256) void iir_forward_fgi_kernel(const v2f *__restrict__ in,
+                                                              v2f *__restrict__ yf, StageGeom g,
+                                                              Sos32 c) {
+  const WaveCtx w = wave_ctx(g);
+  if (!w.valid) return;
   const int n = g.n, e = n + 2 * kPad;
-  const v2f *__restrict__ x = in + (int64_t)f * in_stride;
-  v2f *__restrict__ y = yf + (int64_t)f * yf_stride;
-
-  auto X = [&](int i) -> v2f {
-    v2f v = x[i];
-    if constexpr (MIX) v = cmul(v, lo[i]);
-    return v;
+  const v2f *__restrict__ x = in + fgi(w.fg, n, 0) + w.lane;
+  v2f *__restrict__ y = yf + fgi(w.fg, e, 0) + w.lane;
+  auto X = [&](int i) -> v2f { return x[(int64_t)i << 6]; };
+  auto ext = [&](int j) -> v2f {  // wave-uniform branch on j
+    if (j < kPad) return 2.f * X(0) - X(kPad - j);
+    if (j < n + kPad) return X(j - kPad);
+    return 2.f * X(n - 1) - X(2 * n + kPad - 2 - j);
   };
-
-  const int j0 = b * g.block;
-  const int j1 = min(j0 + g.block, e);
   IirState s;
   int js;
-  if (j0 - g.warmup <= 0) {
+  if (w.j0 - g.warmup <= 0) {
     js = 0;
-    state_steady(s, c, 2.f * X(0) - X(kPad));  // ext[0]
+    state_steady(s, c, ext(0));
   } else {
-    js = j0 - g.warmup;
+    js = w.j0 - g.warmup;
     state_zero(s);
   }
-
+  auto emit = [&](int j, v2f o) { y[(int64_t)j << 6] = o; };
   auto run = [&](int ja, int jb, auto store_tag) {
     constexpr bool STORE = decltype(store_tag)::value;
-    int j = ja;
-    if (j < kPad && j < jb) {  // left odd extension: 2 x[0] - x[27 - j]
-      const v2f x0 = X(0);
-      const int je = min(jb, kPad);
-      for (; j < je; ++j) {
-        v2f o = cascade(2.f * x0 - X(kPad - j), s, c);
-        if constexpr (STORE) y[j] = o;
-      }
+    int a = ja;
+    for (; a < min(jb, kPad); ++a) {  // left odd extension
+      const v2f o = cascade(ext(a), s, c);
+      if constexpr (STORE) emit(a, o);
     }
-    const int je = min(jb, n + kPad);
-#pragma unroll 4
-    for (; j < je; ++j) {
-      v2f o = cascade(X(j - kPad), s, c);
-      if constexpr (STORE) y[j] = o;
+    const int ib = min(jb, n + kPad);
+    if (a < ib) {
+      pipelined_run<STORE>(a, ib, [&](int j) { return X(j - kPad); }, s, c, emit);
+      a = ib;
     }
-    if (j < jb) {  // right odd extension: 2 x[n-1] - x[2n + 25 - j]
-      const v2f xl = X(n - 1);
-      for (; j < jb; ++j) {
-        v2f o = cascade(2.f * xl - X(2 * n + kPad - 2 - j), s, c);
-        if constexpr (STORE) y[j] = o;
-      }
+    for (; a < jb; ++a) {  // right odd extension
+      const v2f o = cascade(ext(a), s, c);
+      if constexpr (STORE) emit(a, o);
     }
   };
-  run(js, j0, std::false_type{});
-  run(j0, j1, std::true_type{});
+  run(js, w.j0, std::false_type{});
+  run(w.j0, w.j1, std::true_type{});
+}
+
+// ------------------------------------------------------------------ forward pass, stage 0
+// Input: the caller's frames in natural layout (frame-major complex64), mixed with the LO
+// table on load.  Lanes are frames, so a direct per-lane load would touch 64 cache lines per
+// instruction; instead each wave stages a 64-frame x 16-sample tile through LDS, loaded
+// with 16 lanes per 128 B frame segment, and the next tile's loads are in flight while the
+// current one is filtered.
+constexpr int kTile = 16;
+constexpr int kTileStride = kTile + 2;  // float2 units: 144 B rows, 16 B aligned, conflict-free
+
+__global__ __launch_bounds__(256) void iir_forward_mix_kernel(const v2f *__restrict__ in,
+                                                              int64_t L, int frames,
+                                                              const v2f *__restrict__ lo,
+                                                              v2f *__restrict__ yf, StageGeom g,
+                                                              Sos32 c) {
+  __shared__ __attribute__((aligned(16))) v2f tile_all[4][64 * kTileStride];
+  const WaveCtx w = wave_ctx(g);
+  if (!w.valid) return;
+  const int n = g.n, e = n + 2 * kPad;  // n == L
+  v2f *tile = tile_all[threadIdx.x >> 6];
+  v2f *__restrict__ y = yf + fgi(w.fg, e, 0) + w.lane;
+  const int f0 = w.fg * 64;
+  // loader geometry: element (row r = 4q + lane/16, col k = lane%16)
+  const int lrow = w.lane >> 4, lcol = w.lane & 15;
+
+  auto xm = [&](int f, int i) -> v2f {  // mixed sample of frame f at index i (natural layout)
+    return cmul(in[(int64_t)f * L + i], lo[i]);
+  };
+  auto ext_slow = [&](int f, int j) -> v2f {
+    if (f >= frames || j < 0 || j >= e) return splat(0.f);
+    if (j < kPad) return 2.f * xm(f, 0) - xm(f, kPad - j);
+    if (j < n + kPad) return xm(f, j - kPad);
+    return 2.f * xm(f, n - 1) - xm(f, 2 * n + kPad - 2 - j);
+  };
+
+  v2f pf[16];  // this lane's share of the next tile
+  auto load_tile = [&](int jc) {
+    const int j = jc + lcol;
+    const bool fast = jc >= kPad && jc + kTile <= n + kPad && f0 + 64 <= frames;  // uniform
+    if (fast) {
+      const v2f l = lo[j - kPad];
+      const v2f *p = in + (int64_t)(f0 + lrow) * L + (j - kPad);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pf[q] = cmul(p[(int64_t)q * 4 * L], l);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pf[q] = ext_slow(f0 + 4 * q + lrow, j);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tile[(4 * q + lrow) * kTileStride + lcol] = pf[q];
+  };
+
+  IirState s;
+  int js;
+  if (w.j0 - g.warmup <= 0) {
+    js = 0;
+    state_steady(s, c, ext_slow(f0 + w.lane, 0));
+  } else {
+    js = w.j0 - g.warmup;
+    state_zero(s);
+  }
+  load_tile(js);
+  for (int jc = js; jc < w.j1; jc += kTile) {
+    store_tile();                       // tile jc (its loads were issued one tile ago)
+    __builtin_amdgcn_wave_barrier();
+    if (jc + kTile < w.j1) load_tile(jc + kTile);  // in flight during the filter below
+    const v2f *row = tile + w.lane * kTileStride;
+    const int steps = min(kTile, w.j1 - jc);
+    if (steps == kTile && jc >= w.j0) {
+#pragma unroll
+      for (int k = 0; k < kTile; ++k) y[(int64_t)(jc + k) << 6] = cascade(row[k], s, c);
+    } else {
+      for (int k = 0; k < steps; ++k) {
+        const v2f o = cascade(row[k], s, c);
+        if (jc + k >= w.j0) y[(int64_t)(jc + k) << 6] = o;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 // ------------------------------------------------------------------ backward pass
-// sosfilt over reversed yf with state zi*yf[e-1]; keep j = 27 + 2m, m in [0, ceil(n/2)).
+// sosfilt over reversed yf with state zi*yf[e-1]; keep j = 27 + 2m -> out(m), FGI layout.
 __global__ __launch_bounds__(256) void iir_backward_kernel(const v2f *__restrict__ yf,
-                                                           int64_t yf_stride,
-                                                           v2f *__restrict__ out,
-                                                           int64_t out_stride, StageGeom g,
-                                                           int frames, Sos32 c) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)frames * g.nblk) return;
-  const int f = (int)(gid / g.nblk);
-  const int b = (int)(gid - (int64_t)f * g.nblk);
-  const int n = g.n, e = n + 2 * kPad;
-  const v2f *__restrict__ y = yf + (int64_t)f * yf_stride;
-  v2f *__restrict__ o = out + (int64_t)f * out_stride;
-
-  const int j0 = b * g.block;
-  const int j1 = min(j0 + g.block, e);
-  const int jlo = max(j0, kPad);          // below kPad: left pad, no outputs -> skipped
-  if (jlo >= j1) return;
+                                                           v2f *__restrict__ out, StageGeom g,
+                                                           Sos32 c) {
+  const WaveCtx w = wave_ctx(g);
+  if (!w.valid) return;
+  const int n = g.n, e = n + 2 * kPad, m_len = (n + 1) >> 1;
+  const v2f *__restrict__ y = yf + fgi(w.fg, e, 0) + w.lane;
+  v2f *__restrict__ o = out + fgi(w.fg, m_len, 0) + w.lane;
+  const int jlo = max(w.j0, kPad);  // below kPad: left pad, no outputs -> skipped
+  if (jlo >= w.j1) return;
+  const int jhi = min(w.j1, n + kPad);  // outputs for j in [jlo, jhi)
   IirState s;
-  int j;
-  if (j1 + g.warmup >= e) {
-    j = e - 1;
-    state_steady(s, c, y[e - 1]);
+  int jt;  // exclusive top of the descending run
+  if (w.j1 + g.warmup >= e) {
+    jt = e;
+    state_steady(s, c, y[(int64_t)(e - 1) << 6]);
   } else {
-    j = j1 - 1 + g.warmup;
+    jt = w.j1 + g.warmup;
     state_zero(s);
   }
-  const int jhi = min(j1, n + kPad) - 1;  // last j with an output candidate
-#pragma unroll 4
-  for (; j > jhi; --j) cascade(y[j], s, c);  // warm-up + right pad
-  if (j >= jlo && ((j - kPad) & 1)) {       // odd m: no output
-    cascade(y[j], s, c);
-    --j;
-  }
-#pragma unroll 2
-  for (; j - 1 >= jlo; j -= 2) {
-    o[(j - kPad) >> 1] = cascade(y[j], s, c);
-    cascade(y[j - 1], s, c);
-  }
-  if (j >= jlo) o[(j - kPad) >> 1] = cascade(y[j], s, c);
+  // descending index d = jt - 1 - j; run over j in (jhi, jt) without output, then [jlo, jhi)
+  auto Y = [&](int j) -> v2f { return y[(int64_t)j << 6]; };
+  auto emit = [&](int d, v2f v) {
+    const int j = jt - 1 - d;
+    if (!((j - kPad) & 1)) o[(int64_t)((j - kPad) >> 1) << 6] = v;
+  };
+  pipelined_run<false>(0, jt - jhi, [&](int d) { return Y(jt - 1 - d); }, s, c, emit);
+  pipelined_run<true>(jt - jhi, jt - jlo, [&](int d) { return Y(jt - 1 - d); }, s, c, emit);
+}
+
+// out[f][i] = in FGI (f, i): for zoomfft's host API
+__global__ __launch_bounds__(256) void deinterleave_kernel(const v2f *__restrict__ in,
+                                                           int64_t len, int frames,
+                                                           v2f *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len * frames) return;
+  const int f = (int)(i / len);
+  const int64_t j = i - (int64_t)f * len;
+  out[i] = in[fgi(f >> 6, len, j) + (f & 63)];
 }
 
 __global__ __launch_bounds__(256) void mix_kernel(const v2f *__restrict__ in,
@@ -254,25 +396,32 @@ __device__ void fft_lds(v2f *sh, int N, int log2n, const v2f *__restrict__ tw, i
 // One workgroup per frame: for each Welch segment, constant detrend + window + N-point
 // FFT in LDS, |X|^2 accumulated in registers for the W cropped bins only; then density
 // scale, fftshift crop and 20*log10 (S:2111-2119).
+// Input either the FGI output of the last decimation stage (stride 64 between samples of a
+// frame) or, at zoom 1, the caller's natural-layout frames.  Frames sharing FGI cache lines
+// (16 consecutive frames per 128 B) are kept on one XCD: blocks b and b + 8 share an XCD.
+template <bool FGI>
 __global__ __launch_bounds__(1024) void welch_rows_kernel(const v2f *__restrict__ x,
-                                                          int64_t x_stride,
+                                                          int64_t len,
                                                           const float *__restrict__ win,
                                                           const v2f *__restrict__ tw,
                                                           WelchGeom g, float *__restrict__ rows,
-                                                          int64_t row_stride) {
+                                                          int frames) {
   extern __shared__ v2f sh[];
   v2f *red = sh + g.n_fft;
   const int T = blockDim.x, tid = threadIdx.x, N = g.n_fft;
-  const v2f *__restrict__ xf = x + (int64_t)blockIdx.x * x_stride;
+  int f = blockIdx.x;
+  if ((frames & 7) == 0) f = (blockIdx.x & 7) * (frames >> 3) + (blockIdx.x >> 3);
+  const int64_t sstride = FGI ? 64 : 1;
+  const v2f *__restrict__ xf = FGI ? x + fgi(f >> 6, len, 0) + (f & 63) : x + (int64_t)f * len;
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 
   for (int s = 0; s < g.nseg; ++s) {
-    const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
+    const v2f *__restrict__ seg = xf + (int64_t)s * g.step * sstride;
     v2f sum = splat(0.f);
     for (int n = tid; n < N; n += T) {
-      const v2f v = n < g.nperseg ? seg[n] : splat(0.f);
+      const v2f v = n < g.nperseg ? seg[n * sstride] : splat(0.f);
       sh[n] = v;
       sum += v;
     }
@@ -299,7 +448,7 @@ __global__ __launch_bounds__(1024) void welch_rows_kernel(const v2f *__restrict_
     }
     __syncthreads();
   }
-  float *__restrict__ row = rows + (int64_t)blockIdx.x * row_stride;
+  float *__restrict__ row = rows + (int64_t)f * g.n_win;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int j = tid + i * T;
@@ -364,28 +513,35 @@ __global__ void waterfall_read_kernel(const float *__restrict__ ring, int H, int
 // ------------------------------------------------------------------ launchers
 static inline unsigned nblocks(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
-hipError_t launch_iir_forward(const float2 *in, int64_t in_stride, const float2 *lo, bool mix,
-                              float2 *yf, int64_t yf_stride, const StageGeom &g, int frames,
-                              hipStream_t st) {
-  const int64_t lanes = (int64_t)frames * g.nblk;
-  const Sos32 c = sos32();
-  if (mix)
-    hipLaunchKernelGGL(iir_forward_kernel<true>, dim3(nblocks(lanes, 256)), dim3(256), 0, st,
-                       (const v2f *)in, in_stride, (const v2f *)lo, (v2f *)yf, yf_stride, g,
-                       frames, c);
-  else
-    hipLaunchKernelGGL(iir_forward_kernel<false>, dim3(nblocks(lanes, 256)), dim3(256), 0, st,
-                       (const v2f *)in, in_stride, (const v2f *)lo, (v2f *)yf, yf_stride, g,
-                       frames, c);
+static inline unsigned wave_blocks(const StageGeom &g) {
+  return (unsigned)(((int64_t)g.ngroups * g.nblk + 3) / 4);
+}
+
+hipError_t launch_iir_forward_mix(const float2 *in, int64_t L, int frames, const float2 *lo,
+                                  float2 *yf, const StageGeom &g, hipStream_t st) {
+  hipLaunchKernelGGL(iir_forward_mix_kernel, dim3(wave_blocks(g)), dim3(256), 0, st,
+                     (const v2f *)in, L, frames, (const v2f *)lo, (v2f *)yf, g, sos32());
   return hipGetLastError();
 }
 
-hipError_t launch_iir_backward(const float2 *yf, int64_t yf_stride, float2 *out,
-                               int64_t out_stride, const StageGeom &g, int frames,
+hipError_t launch_iir_forward_fgi(const float2 *in, float2 *yf, const StageGeom &g,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(iir_forward_fgi_kernel, dim3(wave_blocks(g)), dim3(256), 0, st,
+                     (const v2f *)in, (v2f *)yf, g, sos32());
+  return hipGetLastError();
+}
+
+hipError_t launch_iir_backward(const float2 *yf, float2 *out, const StageGeom &g,
                                hipStream_t st) {
-  const int64_t lanes = (int64_t)frames * g.nblk;
-  hipLaunchKernelGGL(iir_backward_kernel, dim3(nblocks(lanes, 256)), dim3(256), 0, st,
-                     (const v2f *)yf, yf_stride, (v2f *)out, out_stride, g, frames, sos32());
+  hipLaunchKernelGGL(iir_backward_kernel, dim3(wave_blocks(g)), dim3(256), 0, st,
+                     (const v2f *)yf, (v2f *)out, g, sos32());
+  return hipGetLastError();
+}
+
+hipError_t launch_deinterleave(const float2 *in, int64_t len, int frames, float2 *out,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(deinterleave_kernel, dim3(nblocks(len * frames, 256)), dim3(256), 0, st,
+                     (const v2f *)in, len, frames, (v2f *)out);
   return hipGetLastError();
 }
 
@@ -396,21 +552,26 @@ hipError_t launch_mix(const float2 *in, const float2 *lo, float2 *out, int64_t n
   return hipGetLastError();
 }
 
-hipError_t launch_welch_rows(const float2 *x, int64_t x_stride, const float *win,
-                             const float2 *tw, const WelchGeom &g, float *rows,
-                             int64_t row_stride, int frames, hipStream_t st) {
+hipError_t launch_welch_rows(const float2 *x, bool fgi_layout, int64_t len, const float *win,
+                             const float2 *tw, const WelchGeom &g, float *rows, int frames,
+                             hipStream_t st) {
   const int T = g.n_fft / 16 > 64 ? g.n_fft / 16 : 64;  // <= 4 radix-4 butterflies per thread
   const size_t lds = (size_t)(g.n_fft + 32) * sizeof(v2f);
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)welch_rows_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (kMaxLdsFft + 32) * (int)sizeof(v2f));
-    if (e != hipSuccess) return e;
+    for (const void *fn : {(const void *)welch_rows_kernel<true>, (const void *)welch_rows_kernel<false>}) {
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (kMaxLdsFft + 32) * (int)sizeof(v2f));
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
-  hipLaunchKernelGGL(welch_rows_kernel, dim3(frames), dim3(T), lds, st, (const v2f *)x, x_stride,
-                     win, (const v2f *)tw, g, rows, row_stride);
+  if (fgi_layout)
+    hipLaunchKernelGGL(welch_rows_kernel<true>, dim3(frames), dim3(T), lds, st, (const v2f *)x, len,
+                       win, (const v2f *)tw, g, rows, frames);
+  else
+    hipLaunchKernelGGL(welch_rows_kernel<false>, dim3(frames), dim3(T), lds, st, (const v2f *)x,
+                       len, win, (const v2f *)tw, g, rows, frames);
   return hipGetLastError();
 }
 

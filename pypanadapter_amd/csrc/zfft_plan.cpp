@@ -120,15 +120,16 @@ std::vector<int64_t> stage_lengths(int64_t L, int K) {
   return n;
 }
 
-int choose_block(const zfft_plan *p, int64_t e, int frames) {
-  if (p->block_override > 0) return p->block_override;
-  // Enough lanes to fill 256 CUs x 8+ waves; larger blocks amortise the warm-up.
-  int S = 8192;
-  while (S > 512 && (int64_t)frames * ((e + S - 1) / S) < 131072) S >>= 1;
+int choose_block(const zfft_plan *p, int64_t n, int ngroups) {
+  if (p->block_override > 0) return (p->block_override + 15) & ~15;
+  // Enough waves (one per block of a 64-frame group) to fill 256 CUs many times over;
+  // larger blocks amortise the warm-up.
+  int S = 4096;
+  while (S > 512 && (int64_t)ngroups * ((n + kPad + S - 1) / S) < 8192) S >>= 1;
   return S;
 }
 
-int warmup(const zfft_plan *p) { return p->warm_override > 0 ? p->warm_override : 192; }
+int warmup(const zfft_plan *p) { return p->warm_override > 0 ? (p->warm_override + 15) & ~15 : 192; }
 
 int ensure_lo(zfft_plan *p, int64_t L) {
   if (p->lo_len >= L) return ZFFT_OK;
@@ -188,44 +189,39 @@ int check_lengths(const zfft_plan *p, int64_t L, int32_t frames, std::vector<int
   return ZFFT_OK;
 }
 
-// Decimation cascade on frames x L (device), result left in *out / *out_stride.
+// Decimation cascade on frames x L (natural layout in), result in FGI layout in *out.
 int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
-                  const std::vector<int64_t> &n, const float2 **out, int64_t *out_stride,
-                  hipStream_t st) {
-  if (p->K == 0) {
-    *out = d_iq;
-    *out_stride = L;
-    return ZFFT_OK;
-  }
+                  const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   int rc = ensure_lo(p, L);
   if (rc) return rc;
-  hipError_t e = p->yf.ensure((size_t)frames * (L + 2 * kPad) * sizeof(float2));
-  if (e == hipSuccess) e = p->ping.ensure((size_t)frames * n[1] * sizeof(float2));
-  if (e == hipSuccess && p->K > 1) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
+  const int ngroups = (frames + 63) / 64;
+  const size_t G = (size_t)ngroups * 64;
+  hipError_t e = p->yf.ensure(G * (L + 2 * kPad) * sizeof(float2));
+  if (e == hipSuccess) e = p->ping.ensure(G * n[1] * sizeof(float2));
+  if (e == hipSuccess && p->K > 1) e = p->pong.ensure(G * n[2] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   const float2 *cur = d_iq;
-  int64_t cur_stride = L;
   mark(p, st);
   for (int k = 0; k < p->K; ++k) {
-    const int64_t ek = n[k] + 2 * kPad;
     StageGeom g;
     g.n = (int)n[k];
-    g.block = choose_block(p, ek, frames);
-    g.nblk = (int)((ek + g.block - 1) / g.block);
+    g.block = choose_block(p, n[k], ngroups);
+    g.nblk = (int)((n[k] + kPad + g.block - 1) / g.block);
     g.warmup = warmup(p);
-    e = launch_iir_forward(cur, cur_stride, p->lo.as<float2>(), k == 0, p->yf.as<float2>(), ek, g,
-                           frames, st);
+    g.ngroups = ngroups;
+    if (k == 0)
+      e = launch_iir_forward_mix(d_iq, L, frames, p->lo.as<float2>(), p->yf.as<float2>(), g, st);
+    else
+      e = launch_iir_forward_fgi(cur, p->yf.as<float2>(), g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
     mark(p, st);
     float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
-    e = launch_iir_backward(p->yf.as<float2>(), ek, dst, n[k + 1], g, frames, st);
+    e = launch_iir_backward(p->yf.as<float2>(), dst, g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_backward launch");
     mark(p, st);
     cur = dst;
-    cur_stride = n[k + 1];
   }
   *out = cur;
-  *out_stride = cur_stride;
   return ZFFT_OK;
 }
 
@@ -239,12 +235,14 @@ int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, 
   const int nperseg = (int)(Ld < N ? Ld : N);
   rc = ensure_window(p, nperseg);
   if (rc) return rc;
-  const float2 *x;
-  int64_t xs;
+  const float2 *x = d_iq;
   p->n_marks = 0;
-  if (p->K == 0) mark(p, st);
-  rc = run_decimator(p, d_iq, L, frames, n, &x, &xs, st);
-  if (rc) return rc;
+  if (p->K == 0) {
+    mark(p, st);
+  } else {
+    rc = run_decimator(p, d_iq, L, frames, n, &x, st);
+    if (rc) return rc;
+  }
   WelchGeom w;
   w.n_fft = N;
   w.log2n = ilog2(N);
@@ -254,8 +252,8 @@ int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, 
   w.nseg = (int)((Ld - nperseg) / w.step + 1);
   // density scaling 1/(fs*sum(w^2)) and the segment mean (csd average='mean')
   w.scale = (float)(1.0 / (p->cfg.fs * p->win_ss * (double)w.nseg));
-  hipError_t e = launch_welch_rows(x, xs, p->win.as<float>(), p->tw.as<float2>(), w, d_rows,
-                                   p->cfg.n_win, frames, st);
+  hipError_t e = launch_welch_rows(x, p->K > 0, Ld, p->win.as<float>(), p->tw.as<float2>(), w,
+                                   d_rows, frames, st);
   if (e != hipSuccess) return hip_fail(e, "welch_rows launch");
   mark(p, st);
   p->last_row = d_rows + (int64_t)(frames - 1) * p->cfg.n_win;
@@ -282,7 +280,8 @@ int ensure_waterfall(zfft_plan *p) {
   return ZFFT_OK;
 }
 
-hipStream_t pick_stream(zfft_plan *p, void *s) { return s ? (hipStream_t)s : p->stream; }
+// A NULL stream handle means HIP's default (null) stream, as everywhere in HIP.
+hipStream_t pick_stream(zfft_plan *, void *s) { return (hipStream_t)s; }
 
 int enter(zfft_plan *p) {
   if (!p) return fail(ZFFT_EINVAL, "null plan");
@@ -453,7 +452,6 @@ int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t
   e = hipMemcpyAsync(p->in.p, iq, (size_t)L * sizeof(float2), hipMemcpyHostToDevice, p->stream);
   if (e != hipSuccess) return hip_fail(e, "H2D copy");
   const float2 *x;
-  int64_t xs;
   if (p->K == 0) {  // zoomfft(x, 1) still mixes (S:2093-2094)
     rc = ensure_lo(p, L);
     if (rc) return rc;
@@ -463,8 +461,14 @@ int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t
     if (e != hipSuccess) return hip_fail(e, "mix launch");
     x = p->dec.as<float2>();
   } else {
-    rc = run_decimator(p, p->in.as<float2>(), L, 1, n, &x, &xs, p->stream);
+    const float2 *xf;
+    rc = run_decimator(p, p->in.as<float2>(), L, 1, n, &xf, p->stream);
     if (rc) return rc;
+    e = p->dec.ensure((size_t)n[p->K] * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "allocation failed");
+    e = launch_deinterleave(xf, n[p->K], 1, p->dec.as<float2>(), p->stream);
+    if (e != hipSuccess) return hip_fail(e, "deinterleave launch");
+    x = p->dec.as<float2>();
   }
   const int64_t m = n[p->K];
   e = hipMemcpyAsync(out_iq, x, (size_t)m * sizeof(float2), hipMemcpyDeviceToHost, p->stream);

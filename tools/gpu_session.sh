@@ -33,6 +33,10 @@ for s in $STEPS; do
       run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
       run bench 600 python bench.py --steps 10 --warmup 2 --cpu-seconds 8 || exit $? ;;
+    sweep)
+      for blk in 512 1024 2048 4096; do
+        run sweep_b$blk 300 python bench.py --steps 5 --warmup 1 --no-cpu --block $blk || exit $?
+      done ;;
     bench3)
       run bench_cfg3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu || exit $? ;;
     prof)
