@@ -218,7 +218,7 @@ def main():
     ev_ms_step = ev_max / args.steps * 1e3
     achieved = alg_bytes_step / (ev_ms_step / 1e3) / 1e9
     names = plan.launch_names()
-    moved = stage_bytes(L, zoom, W)
+    moved = [F * b for b in stage_bytes(L, zoom, W)]  # per launch (F frames)
     kernels = {nm: {"ms": round(ms, 4), "design_bytes": b,
                     "GB_per_s": round(b / (ms / 1e3) / 1e9, 1) if ms > 0 else None}
                for nm, ms, b in zip(names, launch_ms, moved)}
