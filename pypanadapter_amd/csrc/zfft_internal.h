@@ -39,10 +39,8 @@ hipError_t launch_iir_forward_mix(const float2 *in, int64_t L, int frames, const
                                   float2 *yf, const StageGeom &g, hipStream_t st);
 hipError_t launch_iir_forward_fgi(const float2 *in, float2 *yf, const StageGeom &g,
                                   hipStream_t st);
-hipError_t launch_iir_backward(const float2 *yf, float2 *out, const StageGeom &g,
-                               hipStream_t st);
-hipError_t launch_deinterleave(const float2 *in, int64_t len, int frames, float2 *out,
-                               hipStream_t st);
+hipError_t launch_iir_backward(const float2 *yf, float2 *out, bool natural, int frames,
+                               const StageGeom &g, hipStream_t st);
 
 struct WelchGeom {
   int n_fft, log2n;
@@ -51,9 +49,8 @@ struct WelchGeom {
   float scale;  // 1 / (fs * sum(w^2) * nseg)
 };
 
-hipError_t launch_welch_rows(const float2 *x, bool fgi_layout, int64_t len, const float *win,
-                             const float2 *tw, const WelchGeom &g, float *rows, int frames,
-                             hipStream_t st);
+hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, const float2 *tw,
+                             const WelchGeom &g, float *rows, int frames, hipStream_t st);
 
 hipError_t launch_waterfall_init(float *ring, int H, int W, hipStream_t st);
 hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,

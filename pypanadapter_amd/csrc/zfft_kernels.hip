@@ -271,15 +271,23 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(const v2f *__restr
 }
 
 // ------------------------------------------------------------------ backward pass
-// sosfilt over reversed yf with state zi*yf[e-1]; keep j = 27 + 2m -> out(m), FGI layout.
+// sosfilt over reversed yf with state zi*yf[e-1]; keep j = 27 + 2m -> out(m).  Output in
+// FGI layout for the next stage, or (last stage, NATURAL) frame-major for the Welch kernel:
+// then a store instruction scatters 8 B to 64 frames, but it is 1/2 the rate of the loads
+// and L2 merges the lines before they leave the XCD.
+template <bool NATURAL>
 __global__ __launch_bounds__(256) void iir_backward_kernel(const v2f *__restrict__ yf,
                                                            v2f *__restrict__ out, StageGeom g,
-                                                           Sos32 c) {
+                                                           int frames, Sos32 c) {
   const WaveCtx w = wave_ctx(g);
   if (!w.valid) return;
   const int n = g.n, e = n + 2 * kPad, m_len = (n + 1) >> 1;
   const v2f *__restrict__ y = yf + fgi(w.fg, e, 0) + w.lane;
-  v2f *__restrict__ o = out + fgi(w.fg, m_len, 0) + w.lane;
+  const int f = w.fg * 64 + w.lane;
+  v2f *__restrict__ o = NATURAL ? out + (int64_t)min(f, frames - 1) * m_len
+                                : out + fgi(w.fg, m_len, 0) + w.lane;
+  const int64_t ostride = NATURAL ? 1 : 64;
+  const bool store_ok = !NATURAL || f < frames;
   const int jlo = max(w.j0, kPad);  // below kPad: left pad, no outputs -> skipped
   if (jlo >= w.j1) return;
   const int jhi = min(w.j1, n + kPad);  // outputs for j in [jlo, jhi)
@@ -296,21 +304,10 @@ __global__ __launch_bounds__(256) void iir_backward_kernel(const v2f *__restrict
   auto Y = [&](int j) -> v2f { return y[(int64_t)j << 6]; };
   auto emit = [&](int d, v2f v) {
     const int j = jt - 1 - d;
-    if (!((j - kPad) & 1)) o[(int64_t)((j - kPad) >> 1) << 6] = v;
+    if (!((j - kPad) & 1) && store_ok) o[(int64_t)((j - kPad) >> 1) * ostride] = v;
   };
   pipelined_run<false>(0, jt - jhi, [&](int d) { return Y(jt - 1 - d); }, s, c, emit);
   pipelined_run<true>(jt - jhi, jt - jlo, [&](int d) { return Y(jt - 1 - d); }, s, c, emit);
-}
-
-// out[f][i] = in FGI (f, i): for zoomfft's host API
-__global__ __launch_bounds__(256) void deinterleave_kernel(const v2f *__restrict__ in,
-                                                           int64_t len, int frames,
-                                                           v2f *__restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= len * frames) return;
-  const int f = (int)(i / len);
-  const int64_t j = i - (int64_t)f * len;
-  out[i] = in[fgi(f >> 6, len, j) + (f & 63)];
 }
 
 __global__ __launch_bounds__(256) void mix_kernel(const v2f *__restrict__ in,
@@ -330,128 +327,227 @@ __device__ __forceinline__ v2f wave_sum(v2f v) {
   return v;
 }
 
-// Stockham autosort FFT (radix-4 passes, one leading radix-2 pass when log2 N is odd),
-// natural-order in and out, in LDS with register staging (one buffer).
-// Pass: v_r = a[j + r N/R] * w^{r k}, k = j mod Ns; DFT_R; a[(j-k) R + k + r Ns] = V_r.
-__device__ void fft_lds(v2f *sh, int N, int log2n, const v2f *__restrict__ tw, int tid, int T) {
-  int Ns = 1;
-  if (log2n & 1) {
-    const int nb = N >> 1;
-    v2f a[8], b[8];
+// ---- in-register DFTs (forward, exp(-2 pi i k n / R)) ----
+__device__ __forceinline__ v2f mul_negi(v2f a) { return v2f{a.y, -a.x}; }  // -i * a
+
+template <int R>
+__device__ __forceinline__ void dft(v2f *v);
+
+template <>
+__device__ __forceinline__ void dft<2>(v2f *v) {
+  const v2f a = v[0], b = v[1];
+  v[0] = a + b;
+  v[1] = a - b;
+}
+
+template <>
+__device__ __forceinline__ void dft<4>(v2f *v) {
+  const v2f a0 = v[0] + v[2], a1 = v[0] - v[2], a2 = v[1] + v[3], a3 = mul_negi(v[1] - v[3]);
+  v[0] = a0 + a2;
+  v[1] = a1 + a3;
+  v[2] = a0 - a2;
+  v[3] = a1 - a3;
+}
+
+// W_16^m for m = 0..15 as compile-time constants
+__device__ __forceinline__ v2f w16(int m) {
+  constexpr float c1 = 0.92387953251128674f, s1 = 0.38268343236508977f, h = 0.70710678118654752f;
+  const float cs[16][2] = {{1.f, 0.f},  {c1, -s1},  {h, -h},    {s1, -c1}, {0.f, -1.f}, {-s1, -c1},
+                           {-h, -h},    {-c1, -s1}, {-1.f, 0.f}, {-c1, s1}, {-h, h},     {-s1, c1},
+                           {0.f, 1.f},  {s1, c1},   {h, h},      {c1, s1}};
+  return v2f{cs[m & 15][0], cs[m & 15][1]};
+}
+
+// n = n2 + 2*n1 (n1 < 4): inner DFT4 over n1, twiddle W8^(n2 k1), outer DFT2 -> X[k1 + 4 k2]
+template <>
+__device__ __forceinline__ void dft<8>(v2f *v) {
+  v2f a[2][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int j = tid + i * T;
-      if (j < nb) { a[i] = sh[j]; b[i] = sh[j + nb]; }
-    }
-    __syncthreads();
+  for (int n2 = 0; n2 < 2; ++n2) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int j = tid + i * T;
-      if (j < nb) {
-        sh[2 * j] = a[i] + b[i];
-        sh[2 * j + 1] = a[i] - b[i];
-      }
-    }
-    __syncthreads();
-    Ns = 2;
+    for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[n2 + 2 * n1];
+    dft<4>(a[n2]);
   }
-  const int q = N >> 2;
-  for (; Ns < N; Ns <<= 2) {
-    v2f v[4][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = tid + i * T;
-      if (j < q) {
+  for (int k1 = 1; k1 < 4; ++k1) a[1][k1] = cmul(a[1][k1], w16(2 * k1));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[i][r] = sh[j + r * q];
-      }
-    }
-    __syncthreads();
-    const int tstride = N / (4 * Ns);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = tid + i * T;
-      if (j < q) {
-        const int k = j & (Ns - 1);
-        v2f v0 = v[i][0], v1 = v[i][1], v2 = v[i][2], v3 = v[i][3];
-        if (Ns > 1) {
-          const int t = k * tstride;
-          v1 = cmul(v1, tw[t]);
-          v2 = cmul(v2, tw[2 * t]);
-          v3 = cmul(v3, tw[3 * t]);
-        }
-        const v2f a0 = v0 + v2, a1 = v0 - v2, a2 = v1 + v3, d = v1 - v3;
-        const v2f a3 = v2f{d.y, -d.x};  // -i * (v1 - v3)
-        const int idx = ((j - k) << 2) + k;
-        sh[idx] = a0 + a2;
-        sh[idx + Ns] = a1 + a3;
-        sh[idx + 2 * Ns] = a0 - a2;
-        sh[idx + 3 * Ns] = a1 - a3;
-      }
-    }
-    __syncthreads();
+  for (int k1 = 0; k1 < 4; ++k1) {
+    v[k1] = a[0][k1] + a[1][k1];
+    v[k1 + 4] = a[0][k1] - a[1][k1];
   }
 }
 
-// One workgroup per frame: for each Welch segment, constant detrend + window + N-point
-// FFT in LDS, |X|^2 accumulated in registers for the W cropped bins only; then density
-// scale, fftshift crop and 20*log10 (S:2111-2119).
-// Input either the FGI output of the last decimation stage (stride 64 between samples of a
-// frame) or, at zoom 1, the caller's natural-layout frames.  Frames sharing FGI cache lines
-// (16 consecutive frames per 128 B) are kept on one XCD: blocks b and b + 8 share an XCD.
-template <bool FGI>
-__global__ __launch_bounds__(1024) void welch_rows_kernel(const v2f *__restrict__ x,
-                                                          int64_t len,
+// n = n2 + 4*n1: inner DFT4 over n1, twiddle W16^(n2 k1), outer DFT4 over n2 -> X[k1 + 4 k2]
+template <>
+__device__ __forceinline__ void dft<16>(v2f *v) {
+  v2f a[4][4];
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[n2 + 4 * n1];
+    dft<4>(a[n2]);
+  }
+#pragma unroll
+  for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1) a[n2][k1] = cmul(a[n2][k1], w16(n2 * k1));
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    v2f b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
+    dft<4>(b);
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
+  }
+}
+
+// LDS index with one pad slot per 16 (breaks the power-of-two strides of the passes)
+__device__ __forceinline__ int lp(int i) { return i + (i >> 4); }
+
+// One Stockham DIT pass of radix R over N points.  Thread t holds 16 values: butterflies
+// u = 0 .. 16/R-1 at j = t + u*N/16, inputs v[u + (16/R) r] = a[j + r N/R].
+// Twiddle v_r *= W_N^(r k N/(R Ns)), k = j mod Ns; outputs a[(j-k) R + k + r Ns].
+template <int R>
+__device__ __forceinline__ void stockham_pass(v2f *v, int t, int N, int Ns,
+                                              const v2f *__restrict__ tw) {
+  constexpr int B = 16 / R;
+#pragma unroll
+  for (int u = 0; u < B; ++u) {
+    const int j = t + u * (N >> 4);
+    const int k = j & (Ns - 1);
+    v2f w[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) w[r] = v[u + B * r];
+    if (Ns > 1) {
+      const int ts = k * (N / (R * Ns));
+#pragma unroll
+      for (int r = 1; r < R; ++r) w[r] = cmul(w[r], tw[r * ts]);
+    }
+    dft<R>(w);
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[u + B * r] = w[r];
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void stockham_store(const v2f *v, v2f *sh, int t, int N, int Ns) {
+  constexpr int B = 16 / R;
+#pragma unroll
+  for (int u = 0; u < B; ++u) {
+    const int j = t + u * (N >> 4);
+    const int k = j & (Ns - 1);
+    const int base = (j - k) * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) sh[lp(base + r * Ns)] = v[u + B * r];
+  }
+}
+
+template <int R>
+__device__ __forceinline__ int stockham_out_index(int t, int N, int Ns, int i) {
+  constexpr int B = 16 / R;
+  const int u = i % B, r = i / B;
+  const int j = t + u * (N >> 4);
+  const int k = j & (Ns - 1);
+  return (j - k) * R + k + r * Ns;
+}
+
+// One workgroup (N/16 threads) per frame.  Per Welch segment (S:2111 -> scipy welch):
+// the 16 samples a thread loads are exactly its first-pass butterfly inputs, so the
+// constant detrend and the window are applied in registers before the first radix-R0
+// pass; then radix-16 Stockham passes through LDS; the last pass accumulates |X|^2 in
+// registers for every bin the thread owns.  The next segment's loads are issued before
+// the current FFT (register prefetch).  Finally: density scale, fftshift crop, 20 log10.
+template <int R0, bool PF, int MAXT>  // PF: register prefetch of the next segment
+__global__ __launch_bounds__(MAXT) void welch_rows_kernel(const v2f *__restrict__ x, int64_t len,
                                                           const float *__restrict__ win,
                                                           const v2f *__restrict__ tw,
                                                           WelchGeom g, float *__restrict__ rows,
                                                           int frames) {
   extern __shared__ v2f sh[];
-  v2f *red = sh + g.n_fft;
-  const int T = blockDim.x, tid = threadIdx.x, N = g.n_fft;
+  const int N = g.n_fft, T = blockDim.x, t = threadIdx.x;
+  const int T16 = N >> 4;          // threads doing butterflies
+  const bool act = t < T16;
+  v2f *red = sh + lp(N);
   int f = blockIdx.x;
-  if ((frames & 7) == 0) f = (blockIdx.x & 7) * (frames >> 3) + (blockIdx.x >> 3);
-  const int64_t sstride = FGI ? 64 : 1;
-  const v2f *__restrict__ xf = FGI ? x + fgi(f >> 6, len, 0) + (f & 63) : x + (int64_t)f * len;
+  if ((frames & 7) == 0 && frames >= 64)  // spread consecutive frames over the 8 XCDs evenly
+    f = (blockIdx.x & 7) * (frames >> 3) + (blockIdx.x >> 3);
+  const v2f *__restrict__ xf = x + (int64_t)f * len;
+
+  auto load_seg = [&](v2f *dst, int s) {
+    const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = t + i * T16;
+      dst[i] = (act && n < g.nperseg) ? seg[n] : splat(0.f);
+    }
+  };
+  v2f pf[16];
+  if constexpr (PF) load_seg(pf, 0);
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 
   for (int s = 0; s < g.nseg; ++s) {
-    const v2f *__restrict__ seg = xf + (int64_t)s * g.step * sstride;
-    v2f sum = splat(0.f);
-    for (int n = tid; n < N; n += T) {
-      const v2f v = n < g.nperseg ? seg[n * sstride] : splat(0.f);
-      sh[n] = v;
-      sum += v;
+    v2f v[16];
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = pf[i];
+      if (s + 1 < g.nseg) load_seg(pf, s + 1);  // in flight during this segment's FFT
+    } else {
+      load_seg(v, s);
     }
+    v2f sum = splat(0.f);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sum += v[i];
+    // constant detrend: block mean over the nperseg samples
     sum = wave_sum(sum);
-    if ((tid & 63) == 0) red[tid >> 6] = sum;
+    if ((t & 63) == 0) red[t >> 6] = sum;
     __syncthreads();
-    if (tid < 64) {
-      v2f t = tid < (T >> 6) ? red[tid] : splat(0.f);
-      t = wave_sum(t);
-      if (tid == 0) red[16] = t;
+    if (t < 64) {
+      v2f q = t < ((T + 63) >> 6) ? red[t] : splat(0.f);
+      q = wave_sum(q);
+      if (t == 0) red[16] = q;
     }
     __syncthreads();
     const v2f mean = red[16] * (1.f / (float)g.nperseg);
-    for (int n = tid; n < g.nperseg; n += T) sh[n] = (sh[n] - mean) * win[n];
-    __syncthreads();
-    fft_lds(sh, N, g.log2n, tw, tid, T);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int j = tid + i * T;
-      if (j < g.n_win) {
-        const v2f v = sh[(j - (g.n_win >> 1)) & (N - 1)];
-        acc[i] = fmaf(v.x, v.x, fmaf(v.y, v.y, acc[i]));
-      }
+    for (int i = 0; i < 16; ++i) {  // zero-pad slots (n >= nperseg) get window 0
+      const int n = t + i * T16;
+      v[i] = (v[i] - mean) * ((act && n < g.nperseg) ? win[n] : 0.f);
     }
-    __syncthreads();
+
+    int Ns = 1;
+    if (act) {
+      stockham_pass<R0>(v, t, N, 1, tw);
+      if (N > R0) stockham_store<R0>(v, sh, t, N, 1);
+    }
+    Ns = R0;
+    while (Ns < N) {
+      __syncthreads();
+      if (act) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = sh[lp(t + r * T16)];
+        stockham_pass<16>(v, t, N, Ns, tw);
+      }
+      if (Ns * 16 < N) {
+        __syncthreads();
+        if (act) stockham_store<16>(v, sh, t, N, Ns);
+      }
+      Ns *= 16;
+    }
+    if (act) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = fmaf(v[i].x, v[i].x, fmaf(v[i].y, v[i].y, acc[i]));
+    }
+    __syncthreads();  // LDS reads of this segment done before the next one writes
   }
+  // bins owned by this thread: output positions of the last pass
+  if (!act) return;
   float *__restrict__ row = rows + (int64_t)f * g.n_win;
+  const int lastNs = N == R0 ? 1 : N / 16;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int j = tid + i * T;
+    const int k = N == R0 ? stockham_out_index<R0>(t, N, 1, i) : stockham_out_index<16>(t, N, lastNs, i);
+    const int j = (k + (g.n_win >> 1)) & (N - 1);  // fftshift + crop: row[j] = P[(j - W/2) mod N]
     if (j < g.n_win) row[j] = 20.f * log10f(acc[i] * g.scale);
   }
 }
@@ -531,17 +627,14 @@ hipError_t launch_iir_forward_fgi(const float2 *in, float2 *yf, const StageGeom 
   return hipGetLastError();
 }
 
-hipError_t launch_iir_backward(const float2 *yf, float2 *out, const StageGeom &g,
-                               hipStream_t st) {
-  hipLaunchKernelGGL(iir_backward_kernel, dim3(wave_blocks(g)), dim3(256), 0, st,
-                     (const v2f *)yf, (v2f *)out, g, sos32());
-  return hipGetLastError();
-}
-
-hipError_t launch_deinterleave(const float2 *in, int64_t len, int frames, float2 *out,
-                               hipStream_t st) {
-  hipLaunchKernelGGL(deinterleave_kernel, dim3(nblocks(len * frames, 256)), dim3(256), 0, st,
-                     (const v2f *)in, len, frames, (v2f *)out);
+hipError_t launch_iir_backward(const float2 *yf, float2 *out, bool natural, int frames,
+                               const StageGeom &g, hipStream_t st) {
+  if (natural)
+    hipLaunchKernelGGL(iir_backward_kernel<true>, dim3(wave_blocks(g)), dim3(256), 0, st,
+                       (const v2f *)yf, (v2f *)out, g, frames, sos32());
+  else
+    hipLaunchKernelGGL(iir_backward_kernel<false>, dim3(wave_blocks(g)), dim3(256), 0, st,
+                       (const v2f *)yf, (v2f *)out, g, frames, sos32());
   return hipGetLastError();
 }
 
@@ -552,27 +645,44 @@ hipError_t launch_mix(const float2 *in, const float2 *lo, float2 *out, int64_t n
   return hipGetLastError();
 }
 
-hipError_t launch_welch_rows(const float2 *x, bool fgi_layout, int64_t len, const float *win,
-                             const float2 *tw, const WelchGeom &g, float *rows, int frames,
-                             hipStream_t st) {
-  const int T = g.n_fft / 16 > 64 ? g.n_fft / 16 : 64;  // <= 4 radix-4 butterflies per thread
-  const size_t lds = (size_t)(g.n_fft + 32) * sizeof(v2f);
+template <int R0, bool PF, int MAXT>
+static hipError_t welch_launch_t(const float2 *x, int64_t len, const float *win,
+                                 const float2 *tw, const WelchGeom &g, float *rows, int frames,
+                                 hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void *fn : {(const void *)welch_rows_kernel<true>, (const void *)welch_rows_kernel<false>}) {
-      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (kMaxLdsFft + 32) * (int)sizeof(v2f));
-      if (e != hipSuccess) return e;
-    }
+    hipError_t e = hipFuncSetAttribute((const void *)welch_rows_kernel<R0, PF, MAXT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (kMaxLdsFft + kMaxLdsFft / 16 + 32) * (int)sizeof(v2f));
+    if (e != hipSuccess) return e;
     attr_set = true;
   }
-  if (fgi_layout)
-    hipLaunchKernelGGL(welch_rows_kernel<true>, dim3(frames), dim3(T), lds, st, (const v2f *)x, len,
-                       win, (const v2f *)tw, g, rows, frames);
-  else
-    hipLaunchKernelGGL(welch_rows_kernel<false>, dim3(frames), dim3(T), lds, st, (const v2f *)x,
-                       len, win, (const v2f *)tw, g, rows, frames);
+  const int T = g.n_fft / 16 > 64 ? g.n_fft / 16 : 64;
+  const size_t lds = (size_t)(g.n_fft + g.n_fft / 16 + 32) * sizeof(v2f);
+  hipLaunchKernelGGL((welch_rows_kernel<R0, PF, MAXT>), dim3(frames), dim3(T), lds, st, (const v2f *)x,
+                     len, win, (const v2f *)tw, g, rows, frames);
   return hipGetLastError();
+}
+
+template <int R0>
+static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
+                               const WelchGeom &g, float *rows, int frames, hipStream_t st) {
+  // threads = N/16 (>= 64): N <= 4096 -> <= 256 threads, room for the prefetch registers
+  if (g.n_fft <= 4096) return welch_launch_t<R0, true, 256>(x, len, win, tw, g, rows, frames, st);
+  if (g.n_fft <= 8192) return welch_launch_t<R0, false, 512>(x, len, win, tw, g, rows, frames, st);
+  return welch_launch_t<R0, false, 1024>(x, len, win, tw, g, rows, frames, st);
+}
+
+// x: natural layout, frame f at x + f*len (the caller's frames at zoom 1, otherwise the
+// last decimation stage's output).  N = R0 * 16^p.
+hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, const float2 *tw,
+                             const WelchGeom &g, float *rows, int frames, hipStream_t st) {
+  switch (g.log2n % 4) {
+    case 0: return welch_launch<16>(x, len, win, tw, g, rows, frames, st);
+    case 1: return welch_launch<2>(x, len, win, tw, g, rows, frames, st);
+    case 2: return welch_launch<4>(x, len, win, tw, g, rows, frames, st);
+    default: return welch_launch<8>(x, len, win, tw, g, rows, frames, st);
+  }
 }
 
 hipError_t launch_waterfall_init(float *ring, int H, int W, hipStream_t st) {

@@ -189,7 +189,8 @@ int check_lengths(const zfft_plan *p, int64_t L, int32_t frames, std::vector<int
   return ZFFT_OK;
 }
 
-// Decimation cascade on frames x L (natural layout in), result in FGI layout in *out.
+// Decimation cascade on frames x L (natural layout in); intermediates in FGI layout, the
+// result (last stage) in natural layout in *out.
 int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
                   const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   int rc = ensure_lo(p, L);
@@ -216,7 +217,7 @@ int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
     if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
     mark(p, st);
     float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
-    e = launch_iir_backward(p->yf.as<float2>(), dst, g, st);
+    e = launch_iir_backward(p->yf.as<float2>(), dst, k == p->K - 1, frames, g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_backward launch");
     mark(p, st);
     cur = dst;
@@ -252,8 +253,8 @@ int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, 
   w.nseg = (int)((Ld - nperseg) / w.step + 1);
   // density scaling 1/(fs*sum(w^2)) and the segment mean (csd average='mean')
   w.scale = (float)(1.0 / (p->cfg.fs * p->win_ss * (double)w.nseg));
-  hipError_t e = launch_welch_rows(x, p->K > 0, Ld, p->win.as<float>(), p->tw.as<float2>(), w,
-                                   d_rows, frames, st);
+  hipError_t e = launch_welch_rows(x, Ld, p->win.as<float>(), p->tw.as<float2>(), w, d_rows,
+                                   frames, st);
   if (e != hipSuccess) return hip_fail(e, "welch_rows launch");
   mark(p, st);
   p->last_row = d_rows + (int64_t)(frames - 1) * p->cfg.n_win;
@@ -461,14 +462,8 @@ int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t
     if (e != hipSuccess) return hip_fail(e, "mix launch");
     x = p->dec.as<float2>();
   } else {
-    const float2 *xf;
-    rc = run_decimator(p, p->in.as<float2>(), L, 1, n, &xf, p->stream);
+    rc = run_decimator(p, p->in.as<float2>(), L, 1, n, &x, p->stream);
     if (rc) return rc;
-    e = p->dec.ensure((size_t)n[p->K] * sizeof(float2));
-    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "allocation failed");
-    e = launch_deinterleave(xf, n[p->K], 1, p->dec.as<float2>(), p->stream);
-    if (e != hipSuccess) return hip_fail(e, "deinterleave launch");
-    x = p->dec.as<float2>();
   }
   const int64_t m = n[p->K];
   e = hipMemcpyAsync(out_iq, x, (size_t)m * sizeof(float2), hipMemcpyDeviceToHost, p->stream);
