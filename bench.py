@@ -111,19 +111,6 @@ def make_frames(torch, F, L, cfg, device, seed):
     return x
 
 
-def stage_bytes(L, zoom, W):
-    """Bytes each launch of the current design moves (intermediates included)."""
-    out, n = [], L
-    for _ in range(int(math.log2(zoom))):
-        e = n + 54
-        m = (n + 1) // 2
-        out.append(8 * n + 8 * e)   # forward: read stage input, write yf
-        out.append(8 * e + 8 * m)   # backward: read yf, write decimated output
-        n = m
-    out.append(8 * n + 4 * W)       # welch: read decimated frame (+overlap in cache), row out
-    return out
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,6 +120,7 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="frames per rank (default: config)")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--warm", type=int, default=0)
+    ap.add_argument("--path", type=int, default=0, help="0 auto, 1 exact order, 2 fused interior")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -164,6 +152,8 @@ def main():
     plan = ZoomFFT(N, zoom, fs, n_win=W, device=local)
     if args.block or args.warm:
         plan.tune(args.block, args.warm)
+    if args.path:
+        plan.set_path(args.path)
     stream = torch.cuda.Stream(dev)  # a real stream: the null stream's handle (0) would be
     torch.cuda.set_stream(stream)    # read by the C-ABI as "the plan's own stream"
     sp = stream.cuda_stream
@@ -218,11 +208,10 @@ def main():
     ev_ms_step = ev_max / args.steps * 1e3
     achieved = alg_bytes_step / (ev_ms_step / 1e3) / 1e9
     names = plan.launch_names()
-    moved = [F * b for b in stage_bytes(L, zoom, W)]  # per launch (F frames)
-    kernels = {nm: {"ms": round(ms, 4), "design_bytes": b,
-                    "GB_per_s": round(b / (ms / 1e3) / 1e9, 1) if ms > 0 else None}
-               for nm, ms, b in zip(names, launch_ms, moved)}
-    dominant = max(kernels, key=lambda k: kernels[k]["ms"]) if kernels else None
+    kernels = {}
+    for i, (nm, ms) in enumerate(zip(names, launch_ms)):
+        kernels[f"{i}:{nm}"] = round(ms, 4)
+    dominant = max(kernels, key=lambda k: kernels[k]) if kernels else None
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath):

@@ -121,6 +121,13 @@ int zfft_plan_tune(zfft_plan *plan, int32_t block, int32_t warmup);
  * forward and backward pass, then the Welch-row kernel.  Diagnostics; adds event records. */
 int zfft_plan_timing(zfft_plan *plan, int32_t enable);
 int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *count);
+/* Comma-separated names of the intervals zfft_plan_timings returns (owned by the plan). */
+const char *zfft_plan_timing_names(zfft_plan *plan);
+
+/* Decimator schedule: 0 = automatic, 1 = exact reference pass order for the whole frame,
+ * 2 = fused commuted-order interior + exact edges (used when windows are small).  Both
+ * produce the reference's rows within the fp32 parity gate; diagnostics / A-B only. */
+int zfft_plan_path(zfft_plan *plan, int32_t path);
 
 const char *zfft_last_error(void);
 int zfft_device_count(void);

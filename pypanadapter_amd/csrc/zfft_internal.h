@@ -42,6 +42,20 @@ hipError_t launch_iir_forward_fgi(const float2 *in, float2 *yf, const StageGeom 
 hipError_t launch_iir_backward(const float2 *yf, float2 *out, bool natural, int frames,
                                const StageGeom &g, hipStream_t st);
 
+// Fused interior pass pair (commuted stage order, zfft_kernels.hip fused_pass_kernel).
+struct FusedGeom {
+  int in_len;   // FGI input length (with pads when in_off > 0)
+  int in_off;   // 27 when the input is in padded "ext" coordinates, else 0
+  int n_mid;    // decimated length ceil((in_len - 2*in_off) / 2) = output length
+  int block;    // S in output units (multiple of 16)
+  int nblk;     // ceil(n_mid / S)
+  int w1, w2;   // warm-up of pass 1 (input rate) and pass 2 (output rate)
+  int ngroups;  // 64-frame groups
+};
+
+hipError_t launch_fused_pass(const float2 *in, float2 *out, bool desc, bool two, bool nat,
+                             const FusedGeom &g, int frames, hipStream_t st);
+
 struct WelchGeom {
   int n_fft, log2n;
   int n_win;

@@ -310,6 +310,139 @@ __global__ __launch_bounds__(256) void iir_backward_kernel(const v2f *__restrict
   pipelined_run<true>(jt - jhi, jt - jlo, [&](int d) { return Y(jt - 1 - d); }, s, c, emit);
 }
 
+// ------------------------------------------------------------------ fused interior passes
+// The interior of each zero-phase stage is LTI, so its forward (C) and backward (A) passes
+// commute; ordering them C0 A0 | A1 C1 | C2 A2 | A3 C3 ... makes neighbouring passes of
+// consecutive stages run in the same direction, and this kernel runs such a pair in one
+// sweep: pass 1 over the input at rate n_k, every other output of it (the ↓2 sample) feeds
+// pass 2 at rate n_{k+1}; only pass 2's output reaches memory.  Without pass 2 (TWO =
+// false) the decimated pass-1 output is stored (last stage, NAT = frame-major for Welch,
+// written through an LDS transpose).  Frame edges are not reproduced here (different
+// order, no odd padding): the host overwrites the edge outputs with an exact computation.
+// Blocks partition the output index m; pass 1 starts w1 input samples (pass 2: w2 mid
+// samples) outside the block with a zero state, or at the sequence end with zi * x.
+template <bool DESC, bool TWO, bool NAT>
+__global__ __launch_bounds__(256) void fused_pass_kernel(const v2f *__restrict__ in,
+                                                         v2f *__restrict__ out, FusedGeom g,
+                                                         int frames, Sos32 c) {
+  __shared__ __attribute__((aligned(16))) v2f tile_all[NAT ? 4 : 1][NAT ? 64 * kTileStride : 1];
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= g.ngroups * g.nblk) return;
+  const int b = wid % g.nblk, fg = wid / g.nblk;
+  const v2f *__restrict__ x = in + fgi(fg, g.in_len, 0) + lane;
+  auto IN = [&](int j) -> v2f { return x[(int64_t)j << 6]; };
+  const int nk = g.in_len - 2 * g.in_off;
+  const int m0 = b * g.block, m1 = min(m0 + g.block, g.n_mid);
+  v2f *__restrict__ o = out + fgi(fg, g.n_mid, 0) + lane;  // FGI output (TWO or !NAT)
+  v2f *tile = tile_all[NAT ? (threadIdx.x >> 6) : 0];
+  const int f0 = fg * 64;
+
+  IirState s1, s2;
+  bool p2_pending = false;
+  int j_first, count, mlo, mhi;  // input steps j_first + dir*q, q < count; emit m in [mlo, mhi]
+  if constexpr (DESC) {
+    const int mt = TWO ? min(m1 + g.w2, g.n_mid) : m1;  // pass-2 exclusive top
+    const int J1 = g.in_off + 2 * (mt - 1) + 1;
+    if (J1 + g.w1 >= g.in_len - 1) {
+      j_first = g.in_len - 1;
+      state_steady(s1, c, IN(j_first));
+    } else {
+      j_first = J1 + g.w1;
+      state_zero(s1);
+    }
+    count = j_first - (g.in_off + 2 * m0) + 1;
+    mlo = m0;
+    mhi = mt - 1;
+    if (TWO) {
+      if (mt == g.n_mid) p2_pending = true;
+      else state_zero(s2);
+    }
+  } else {
+    const int ms = TWO ? max(0, m0 - g.w2) : m0;
+    if (2 * ms - g.w1 <= 0) {
+      j_first = g.in_off;
+      state_steady(s1, c, IN(j_first));
+    } else {
+      j_first = g.in_off + 2 * ms - g.w1;
+      state_zero(s1);
+    }
+    count = g.in_off + 2 * (m1 - 1) - j_first + 1;
+    mlo = ms;
+    mhi = m1 - 1;
+    if (TWO) {
+      if (ms == 0) p2_pending = true;
+      else state_zero(s2);
+    }
+  }
+  (void)nk;
+
+  auto flush = [&](int mbase) {  // NAT: tile columns [mbase, mbase+16) -> frame rows
+    const int lrow = lane >> 4, lcol = lane & 15;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = 4 * q + lrow, m = mbase + lcol;
+      if (f0 + r < frames && m >= m0 && m < m1)
+        out[(int64_t)(f0 + r) * g.n_mid + m] = tile[r * kTileStride + lcol];
+    }
+  };
+
+  auto step = [&](int q, v2f u) {
+    const v2f y1 = cascade(u, s1, c);
+    const int j = DESC ? j_first - q : j_first + q;
+    const int jr = j - g.in_off;
+    if ((jr & 1) == 0) {  // wave-uniform
+      const int m = jr >> 1;
+      if (m >= mlo && m <= mhi) {
+        if constexpr (TWO) {
+          if (p2_pending) {
+            state_steady(s2, c, y1);
+            p2_pending = false;
+          }
+          const v2f y2 = cascade(y1, s2, c);
+          if (m >= m0 && m < m1) o[(int64_t)m << 6] = y2;
+        } else if constexpr (NAT) {
+          tile[lane * kTileStride + (m & 15)] = y1;
+          const bool last = DESC ? ((m & 15) == 0 || m == m0) : ((m & 15) == 15 || m == m1 - 1);
+          if (last) {
+            __builtin_amdgcn_wave_barrier();
+            flush(m & ~15);
+            __builtin_amdgcn_wave_barrier();
+          }
+        } else {
+          o[(int64_t)m << 6] = y1;
+        }
+      }
+    }
+  };
+
+  // register-pipelined input stream (two groups of kU in flight)
+  const int full = count / kU;
+  int q = 0;
+  if (full > 0) {
+    v2f A[kU], B[kU];
+    auto load = [&](v2f *dst, int q0) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) dst[u] = IN(DESC ? j_first - (q0 + u) : j_first + (q0 + u));
+    };
+    load(A, 0);
+    int gi = 0;
+    while (true) {
+      if (gi + 1 < full) load(B, q + kU);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) step(q + u, A[u]);
+      q += kU;
+      if (++gi >= full) break;
+      if (gi + 1 < full) load(A, q + kU);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) step(q + u, B[u]);
+      q += kU;
+      if (++gi >= full) break;
+    }
+  }
+  for (; q < count; ++q) step(q, IN(DESC ? j_first - q : j_first + q));
+}
+
 __global__ __launch_bounds__(256) void mix_kernel(const v2f *__restrict__ in,
                                                   const v2f *__restrict__ lo,
                                                   v2f *__restrict__ out, int64_t n) {
@@ -635,6 +768,27 @@ hipError_t launch_iir_backward(const float2 *yf, float2 *out, bool natural, int 
   else
     hipLaunchKernelGGL(iir_backward_kernel<false>, dim3(wave_blocks(g)), dim3(256), 0, st,
                        (const v2f *)yf, (v2f *)out, g, frames, sos32());
+  return hipGetLastError();
+}
+
+hipError_t launch_fused_pass(const float2 *in, float2 *out, bool desc, bool two, bool nat,
+                             const FusedGeom &g, int frames, hipStream_t st) {
+  const unsigned blocks = (unsigned)(((int64_t)g.ngroups * g.nblk + 3) / 4);
+  const v2f *i = (const v2f *)in;
+  v2f *o = (v2f *)out;
+  const Sos32 c = sos32();
+  if (desc && two)
+    hipLaunchKernelGGL((fused_pass_kernel<true, true, false>), dim3(blocks), dim3(256), 0, st, i, o, g, frames, c);
+  else if (!desc && two)
+    hipLaunchKernelGGL((fused_pass_kernel<false, true, false>), dim3(blocks), dim3(256), 0, st, i, o, g, frames, c);
+  else if (desc && nat)
+    hipLaunchKernelGGL((fused_pass_kernel<true, false, true>), dim3(blocks), dim3(256), 0, st, i, o, g, frames, c);
+  else if (!desc && nat)
+    hipLaunchKernelGGL((fused_pass_kernel<false, false, true>), dim3(blocks), dim3(256), 0, st, i, o, g, frames, c);
+  else if (desc)
+    hipLaunchKernelGGL((fused_pass_kernel<true, false, false>), dim3(blocks), dim3(256), 0, st, i, o, g, frames, c);
+  else
+    hipLaunchKernelGGL((fused_pass_kernel<false, false, false>), dim3(blocks), dim3(256), 0, st, i, o, g, frames, c);
   return hipGetLastError();
 }
 

@@ -96,20 +96,27 @@ struct zfft_plan {
   bool wf_ready = false;
   const float *last_row = nullptr;  // device row of the last processed frame
   bool timing = false;
-  std::vector<hipEvent_t> events;    // 2 per launch when timing is on
+  std::vector<hipEvent_t> events;    // one per mark when timing is on
+  std::vector<std::string> mark_names;
+  std::string names_buf;
   int n_marks = 0;
+  int path = 0;                      // 0 auto, 1 exact pipeline only, 2 fused when applicable
+  DevBuf edge, xk;
 };
 
 namespace {
 
-// Timing marks: an event before the first launch and after each launch of a call.
-void mark(zfft_plan *p, hipStream_t st) {
+// Timing marks: an event before the first launch and after each launch (or launch group)
+// of a call, with the name of what ran since the previous mark.
+void mark(zfft_plan *p, hipStream_t st, const char *what = "") {
   if (!p->timing) return;
   if ((int)p->events.size() <= p->n_marks) {
     hipEvent_t ev;
     if (hipEventCreate(&ev) != hipSuccess) return;
     p->events.push_back(ev);
   }
+  if ((int)p->mark_names.size() <= p->n_marks) p->mark_names.resize(p->n_marks + 1);
+  p->mark_names[p->n_marks] = what;
   (void)hipEventRecord(p->events[p->n_marks++], st);
 }
 
@@ -189,20 +196,19 @@ int check_lengths(const zfft_plan *p, int64_t L, int32_t frames, std::vector<int
   return ZFFT_OK;
 }
 
-// Decimation cascade on frames x L (natural layout in); intermediates in FGI layout, the
-// result (last stage) in natural layout in *out.
-int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
-                  const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
-  int rc = ensure_lo(p, L);
-  if (rc) return rc;
+// Exact decimation cascade (reference pass order, odd padding, zi initial conditions) on
+// `frames` frames of n[0] samples each at frame stride `stride` (natural layout in; lo points
+// at the LO value of the first sample).  Intermediates in FGI layout, the result (last
+// stage) in natural layout in *out.
+int run_exact(zfft_plan *p, const float2 *in, int64_t stride, const float2 *lo, int frames,
+              const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   const int ngroups = (frames + 63) / 64;
   const size_t G = (size_t)ngroups * 64;
-  hipError_t e = p->yf.ensure(G * (L + 2 * kPad) * sizeof(float2));
+  hipError_t e = p->yf.ensure(G * (n[0] + 2 * kPad) * sizeof(float2));
   if (e == hipSuccess) e = p->ping.ensure(G * n[1] * sizeof(float2));
   if (e == hipSuccess && p->K > 1) e = p->pong.ensure(G * n[2] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
-  const float2 *cur = d_iq;
-  mark(p, st);
+  const float2 *cur = in;
   for (int k = 0; k < p->K; ++k) {
     StageGeom g;
     g.n = (int)n[k];
@@ -211,19 +217,124 @@ int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
     g.warmup = warmup(p);
     g.ngroups = ngroups;
     if (k == 0)
-      e = launch_iir_forward_mix(d_iq, L, frames, p->lo.as<float2>(), p->yf.as<float2>(), g, st);
+      e = launch_iir_forward_mix(in, stride, frames, lo, p->yf.as<float2>(), g, st);
     else
       e = launch_iir_forward_fgi(cur, p->yf.as<float2>(), g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
-    mark(p, st);
+    mark(p, st, k == 0 ? "exact_forward_mix" : "exact_forward");
     float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
     e = launch_iir_backward(p->yf.as<float2>(), dst, k == p->K - 1, frames, g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_backward launch");
-    mark(p, st);
+    mark(p, st, "exact_backward");
     cur = dst;
   }
   *out = cur;
   return ZFFT_OK;
+}
+
+// Edge width (final-stage samples) recomputed exactly, and the exact window length.
+constexpr int kEdge = 384;
+int64_t edge_window(int K) { return ((int64_t)1 << K) * (kEdge + 640); }
+
+bool use_fused(const zfft_plan *p, int64_t L) {
+  if (p->path == 1 || p->K < 2) return false;
+  return 8 * edge_window(p->K) <= L;  // windows cost <= 1/4 of a frame
+}
+
+int fused_block(int64_t n_mid, int ngroups) {
+  int S = 2048;
+  while (S > 256 && (int64_t)ngroups * ((n_mid + S - 1) / S) < 4096) S >>= 1;
+  return S;
+}
+
+// Interior in commuted pass order with fused same-direction pass pairs, edges exact:
+//   [C0] [A0 A1] [C1 C2] [A2 A3] ... [last pass of stage K-1, decimated, natural layout]
+// then the first/last kEdge outputs are replaced by the exact pipeline on prefix/suffix
+// windows of the frames (run first, their edge outputs parked in p->edge).
+int run_fused(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
+              const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
+  const int K = p->K;
+  const int64_t nK = n[K];
+  const int ngroups = (frames + 63) / 64;
+  const size_t G = (size_t)ngroups * 64;
+  const int64_t P = edge_window(K);
+  const int64_t L0 = ((L - P) >> K) << K;  // suffix window start, multiple of 2^K
+  std::vector<int64_t> npre = stage_lengths(P, K), nsuf = stage_lengths(L - L0, K);
+  // all workspace first (the window runs reuse the interior chain's buffers)
+  hipError_t e = p->edge.ensure((size_t)frames * 2 * kEdge * sizeof(float2));
+  if (e == hipSuccess) e = p->xk.ensure((size_t)frames * nK * sizeof(float2));
+  if (e == hipSuccess) e = p->yf.ensure(G * (L + 2 * kPad) * sizeof(float2));
+  if (e == hipSuccess) e = p->ping.ensure(G * n[1] * sizeof(float2));
+  if (e == hipSuccess) e = p->pong.ensure(G * n[2] * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+  float2 *edge = p->edge.as<float2>();
+  // exact edges: prefix window -> cols [0, E), suffix window -> cols [E, 2E)
+  const float2 *w;
+  int rc = run_exact(p, d_iq, L, p->lo.as<float2>(), frames, npre, &w, st);
+  if (rc) return rc;
+  e = hipMemcpy2DAsync(edge, 2 * kEdge * sizeof(float2), w, npre[K] * sizeof(float2),
+                       kEdge * sizeof(float2), frames, hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return hip_fail(e, "edge copy");
+  rc = run_exact(p, d_iq + L0, L, p->lo.as<float2>() + L0, frames, nsuf, &w, st);
+  if (rc) return rc;
+  e = hipMemcpy2DAsync(edge + kEdge, 2 * kEdge * sizeof(float2), w + (nsuf[K] - kEdge),
+                       nsuf[K] * sizeof(float2), kEdge * sizeof(float2), frames,
+                       hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return hip_fail(e, "edge copy");
+  mark(p, st, "edge_windows");
+
+  // interior chain
+  StageGeom g0;
+  g0.n = (int)L;
+  g0.block = choose_block(p, L, ngroups);
+  g0.nblk = (int)((L + kPad + g0.block - 1) / g0.block);
+  g0.warmup = warmup(p);
+  g0.ngroups = ngroups;
+  e = launch_iir_forward_mix(d_iq, L, frames, p->lo.as<float2>(), p->yf.as<float2>(), g0, st);
+  if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
+  mark(p, st, "C0_forward_mix");
+  const float2 *cur = p->yf.as<float2>();
+  int64_t cur_len = L + 2 * kPad;
+  int cur_off = kPad;
+  for (int i = 0; i <= K - 1; ++i) {  // kernel i: 2nd pass of stage i (+ 1st of stage i+1)
+    const bool two = i < K - 1;
+    FusedGeom fg;
+    fg.in_len = (int)cur_len;
+    fg.in_off = cur_off;
+    fg.n_mid = (int)n[i + 1];
+    fg.block = fused_block(fg.n_mid, ngroups);
+    fg.nblk = (fg.n_mid + fg.block - 1) / fg.block;
+    fg.w1 = fg.w2 = warmup(p);
+    fg.ngroups = ngroups;
+    float2 *dst = !two ? p->xk.as<float2>() : ((i & 1) ? p->pong.as<float2>() : p->ping.as<float2>());
+    e = launch_fused_pass(cur, dst, (i & 1) == 0, two, !two, fg, frames, st);
+    if (e != hipSuccess) return hip_fail(e, "fused pass launch");
+    mark(p, st, two ? ((i & 1) ? "fused_asc_pair" : "fused_desc_pair")
+                    : ((i & 1) ? "fused_asc_last" : "fused_desc_last"));
+    cur = dst;
+    cur_len = n[i + 1];
+    cur_off = 0;
+  }
+  // patch the exact edges into the interior result
+  float2 *xk = p->xk.as<float2>();
+  e = hipMemcpy2DAsync(xk, nK * sizeof(float2), edge, 2 * kEdge * sizeof(float2),
+                       kEdge * sizeof(float2), frames, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpy2DAsync(xk + (nK - kEdge), nK * sizeof(float2), edge + kEdge,
+                         2 * kEdge * sizeof(float2), kEdge * sizeof(float2), frames,
+                         hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return hip_fail(e, "edge patch");
+  mark(p, st, "edge_patch");
+  *out = xk;
+  return ZFFT_OK;
+}
+
+int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
+                  const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
+  int rc = ensure_lo(p, L);
+  if (rc) return rc;
+  if (use_fused(p, L)) return run_fused(p, d_iq, L, frames, n, out, st);
+  return run_exact(p, d_iq, L, p->lo.as<float2>(), frames, n, out, st);
 }
 
 int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, float *d_rows,
@@ -238,9 +349,8 @@ int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, 
   if (rc) return rc;
   const float2 *x = d_iq;
   p->n_marks = 0;
-  if (p->K == 0) {
-    mark(p, st);
-  } else {
+  mark(p, st, "start");
+  if (p->K > 0) {
     rc = run_decimator(p, d_iq, L, frames, n, &x, st);
     if (rc) return rc;
   }
@@ -256,7 +366,7 @@ int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, 
   hipError_t e = launch_welch_rows(x, Ld, p->win.as<float>(), p->tw.as<float2>(), w, d_rows,
                                    frames, st);
   if (e != hipSuccess) return hip_fail(e, "welch_rows launch");
-  mark(p, st);
+  mark(p, st, "welch_rows");
   p->last_row = d_rows + (int64_t)(frames - 1) * p->cfg.n_win;
   return ZFFT_OK;
 }
@@ -369,7 +479,7 @@ int zfft_plan_destroy(zfft_plan *p) {
   (void)hipSetDevice(p->cfg.device);
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->yf, &p->ping, &p->pong, &p->rows,
-                    &p->ring, &p->img, &p->one_row, &p->dec})
+                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -391,6 +501,22 @@ int zfft_plan_timing(zfft_plan *p, int32_t enable) {
   p->timing = enable != 0;
   p->n_marks = 0;
   return ZFFT_OK;
+}
+
+int zfft_plan_path(zfft_plan *p, int32_t path) {
+  if (!p || path < 0 || path > 2) return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact) or 2");
+  p->path = path;
+  return ZFFT_OK;
+}
+
+const char *zfft_plan_timing_names(zfft_plan *p) {
+  if (!p) return "";
+  p->names_buf.clear();
+  for (int k = 1; k < p->n_marks; ++k) {
+    if (k > 1) p->names_buf += ",";
+    p->names_buf += p->mark_names[k];
+  }
+  return p->names_buf.c_str();
 }
 
 int zfft_plan_timings(zfft_plan *p, float *ms_out, int32_t max, int32_t *count) {

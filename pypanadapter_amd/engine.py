@@ -90,11 +90,13 @@ class ZoomFFT:
         return [float(buf[i]) for i in range(n.value)]
 
     def launch_names(self) -> list:
-        k = self.zoom.bit_length() - 1
-        names = []
-        for s in range(k):
-            names += [f"iir_forward_s{s}", f"iir_backward_s{s}"]
-        return names + ["welch_rows"]
+        """Names of the intervals `timings()` returns (from the last timed call)."""
+        raw = self.lib.zfft_plan_timing_names(self._plan) or b""
+        return [n for n in raw.decode().split(",") if n]
+
+    def set_path(self, path: int) -> None:
+        """0 auto, 1 exact reference pass order, 2 fused interior + exact edges."""
+        check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
 
     # ---------------------------------------------------------------- DSP
     @staticmethod

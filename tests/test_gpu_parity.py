@@ -147,6 +147,31 @@ def test_device_path_matches_host_path_bitwise():
         assert len(t) == len(plan.launch_names()) and all(v > 0 for v in t)
 
 
+@pytest.mark.parametrize("N,z,L", [(4096, 8, 299008), (1024, 4, 262144), (2048, 16, 300000),
+                                    (1024, 2, 70001), (4096, 32, 1048576)])
+def test_fused_interior_matches_exact_pipeline(oracle_lib, N, z, L):
+    """The fused commuted-order interior + exact edge windows (path 2) against the exact
+    reference-order pipeline (path 1): decimated IQ within fp32 rounding everywhere,
+    including the frame edges, and both rows within the gate of the float64 oracle."""
+    from pypanadapter_amd import ZoomFFT
+    x = _frames(2, L, N, z, N // z, seed0=4200)
+    out = {}
+    for path in (1, 2):
+        with ZoomFFT(N, z, 2.4e6) as plan:
+            plan.set_path(path)
+            out[path] = (plan.rows(x), plan.decimate(x[0]))
+    ref_dec = oracle_lib.zoomfft(x[0], z, 2.4e6)
+    for path in (1, 2):
+        d = out[path][1]
+        assert d.shape == ref_dec.shape
+        err = np.abs(d - ref_dec) / np.abs(ref_dec).max()
+        assert err.max() < 3e-6, (path, float(err.max()), int(err.argmax()), len(d))
+    for f in range(2):
+        ref = oracle_lib.psd_row(x[f], 2.4e6, N, z, N // z)
+        assert_row_close(out[1][0][f], ref, "exact")
+        assert_row_close(out[2][0][f], ref, "fused")
+
+
 def test_size_independent_properties():
     """At larger batches: determinism, frame-order equivariance, exact x2 scaling."""
     from pypanadapter_amd import ZoomFFT
