@@ -498,8 +498,7 @@ int zfft_plan_tune(zfft_plan *p, int32_t block, int32_t warm) {
 
 int zfft_plan_timing(zfft_plan *p, int32_t enable) {
   if (!p) return fail(ZFFT_EINVAL, "null plan");
-  p->timing = enable != 0;
-  p->n_marks = 0;
+  p->timing = enable != 0;  // marks of the last timed call stay readable
   return ZFFT_OK;
 }
 
