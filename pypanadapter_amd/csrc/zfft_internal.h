@@ -33,6 +33,8 @@ struct StageGeom {
   int block;    // S, samples per block (multiple of 16)
   int warmup;   // W, warm-up samples (multiple of 16)
   int ngroups;  // 64-frame groups
+  int split = 0;         // stage 0 only: frame groups >= split read a second window set ...
+  int64_t alt_off = 0;   // ... starting alt_off samples into each frame (edge windows)
 };
 
 hipError_t launch_iir_forward_mix(const float2 *in, int64_t L, int frames, const float2 *lo,

@@ -205,15 +205,20 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(const v2f *__restr
   __shared__ __attribute__((aligned(16))) v2f tile_all[4][64 * kTileStride];
   const WaveCtx w = wave_ctx(g);
   if (!w.valid) return;
-  const int n = g.n, e = n + 2 * kPad;  // n == L
+  const int n = g.n, e = n + 2 * kPad;
   v2f *tile = tile_all[threadIdx.x >> 6];
   v2f *__restrict__ y = yf + fgi(w.fg, e, 0) + w.lane;
-  const int f0 = w.fg * 64;
+  // Frame groups at or above g.split (a multiple of 64, 0 = none) are a second set of
+  // windows starting g.alt_off samples into the same frames (edge windows, one launch).
+  const bool second = g.split > 0 && w.fg * 64 >= g.split;
+  const v2f *__restrict__ inb = in + (second ? g.alt_off : 0);
+  const v2f *__restrict__ lob = lo + (second ? g.alt_off : 0);
+  const int f0 = w.fg * 64 - (second ? g.split : 0);  // frame index of row 0 in its set
   // loader geometry: element (row r = 4q + lane/16, col k = lane%16)
   const int lrow = w.lane >> 4, lcol = w.lane & 15;
 
   auto xm = [&](int f, int i) -> v2f {  // mixed sample of frame f at index i (natural layout)
-    return cmul(in[(int64_t)f * L + i], lo[i]);
+    return cmul(inb[(int64_t)f * L + i], lob[i]);
   };
   auto ext_slow = [&](int f, int j) -> v2f {
     if (f >= frames || j < 0 || j >= e) return splat(0.f);
@@ -227,8 +232,8 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(const v2f *__restr
     const int j = jc + lcol;
     const bool fast = jc >= kPad && jc + kTile <= n + kPad && f0 + 64 <= frames;  // uniform
     if (fast) {
-      const v2f l = lo[j - kPad];
-      const v2f *p = in + (int64_t)(f0 + lrow) * L + (j - kPad);
+      const v2f l = lob[j - kPad];
+      const v2f *p = inb + (int64_t)(f0 + lrow) * L + (j - kPad);
 #pragma unroll
       for (int q = 0; q < 16; ++q) pf[q] = cmul(p[(int64_t)q * 4 * L], l);
     } else {

@@ -200,9 +200,13 @@ int check_lengths(const zfft_plan *p, int64_t L, int32_t frames, std::vector<int
 // `frames` frames of n[0] samples each at frame stride `stride` (natural layout in; lo points
 // at the LO value of the first sample).  Intermediates in FGI layout, the result (last
 // stage) in natural layout in *out.
+// With split > 0 (a multiple of 64) the frames [split, split + frames) are a second window
+// set starting alt_off samples into the same frames; the output then has split + frames rows.
 int run_exact(zfft_plan *p, const float2 *in, int64_t stride, const float2 *lo, int frames,
-              const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
-  const int ngroups = (frames + 63) / 64;
+              const std::vector<int64_t> &n, const float2 **out, hipStream_t st, int split = 0,
+              int64_t alt_off = 0) {
+  const int rows = split > 0 ? split + frames : frames;
+  const int ngroups = (rows + 63) / 64;
   const size_t G = (size_t)ngroups * 64;
   hipError_t e = p->yf.ensure(G * (n[0] + 2 * kPad) * sizeof(float2));
   if (e == hipSuccess) e = p->ping.ensure(G * n[1] * sizeof(float2));
@@ -216,6 +220,8 @@ int run_exact(zfft_plan *p, const float2 *in, int64_t stride, const float2 *lo, 
     g.nblk = (int)((n[k] + kPad + g.block - 1) / g.block);
     g.warmup = warmup(p);
     g.ngroups = ngroups;
+    g.split = split;
+    g.alt_off = alt_off;
     if (k == 0)
       e = launch_iir_forward_mix(in, stride, frames, lo, p->yf.as<float2>(), g, st);
     else
@@ -223,7 +229,7 @@ int run_exact(zfft_plan *p, const float2 *in, int64_t stride, const float2 *lo, 
     if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
     mark(p, st, k == 0 ? "exact_forward_mix" : "exact_forward");
     float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
-    e = launch_iir_backward(p->yf.as<float2>(), dst, k == p->K - 1, frames, g, st);
+    e = launch_iir_backward(p->yf.as<float2>(), dst, k == p->K - 1, rows, g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_backward launch");
     mark(p, st, "exact_backward");
     cur = dst;
@@ -259,7 +265,8 @@ int run_fused(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
   const size_t G = (size_t)ngroups * 64;
   const int64_t P = edge_window(K);
   const int64_t L0 = ((L - P) >> K) << K;  // suffix window start, multiple of 2^K
-  std::vector<int64_t> npre = stage_lengths(P, K), nsuf = stage_lengths(L - L0, K);
+  // both window sets have length Pw = L - L0 in [P, P + 2^K): the suffix ends at the frame end
+  const std::vector<int64_t> npre = stage_lengths(L - L0, K), nsuf = npre;
   // all workspace first (the window runs reuse the interior chain's buffers)
   hipError_t e = p->edge.ensure((size_t)frames * 2 * kEdge * sizeof(float2));
   if (e == hipSuccess) e = p->xk.ensure((size_t)frames * nK * sizeof(float2));
@@ -268,18 +275,19 @@ int run_fused(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
   if (e == hipSuccess) e = p->pong.ensure(G * n[2] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   float2 *edge = p->edge.as<float2>();
-  // exact edges: prefix window -> cols [0, E), suffix window -> cols [E, 2E)
+  // exact edges: one run over prefix windows (rows [0, F)) and suffix windows (rows
+  // [Fp, Fp + F), Fp = F rounded up to 64); then prefix cols [0, E) and suffix cols
+  // [nsuf_K - E, nsuf_K) -> p->edge [F][2E]
+  const int Fp = ngroups * 64;
   const float2 *w;
-  int rc = run_exact(p, d_iq, L, p->lo.as<float2>(), frames, npre, &w, st);
+  int rc = run_exact(p, d_iq, L, p->lo.as<float2>(), frames, npre, &w, st, Fp, L0);
   if (rc) return rc;
   e = hipMemcpy2DAsync(edge, 2 * kEdge * sizeof(float2), w, npre[K] * sizeof(float2),
                        kEdge * sizeof(float2), frames, hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return hip_fail(e, "edge copy");
-  rc = run_exact(p, d_iq + L0, L, p->lo.as<float2>() + L0, frames, nsuf, &w, st);
-  if (rc) return rc;
-  e = hipMemcpy2DAsync(edge + kEdge, 2 * kEdge * sizeof(float2), w + (nsuf[K] - kEdge),
-                       nsuf[K] * sizeof(float2), kEdge * sizeof(float2), frames,
-                       hipMemcpyDeviceToDevice, st);
+  e = hipMemcpy2DAsync(edge + kEdge, 2 * kEdge * sizeof(float2),
+                       w + (int64_t)Fp * npre[K] + (nsuf[K] - kEdge), npre[K] * sizeof(float2),
+                       kEdge * sizeof(float2), frames, hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return hip_fail(e, "edge copy");
   mark(p, st, "edge_windows");
 
