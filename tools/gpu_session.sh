@@ -45,13 +45,15 @@ for s in $STEPS; do
     prof)
       export TMPDIR=/tmp
       run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$OUT/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu || exit $? ;;
+        -d "$OUT/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu || exit $? ;;
     pmc)
       export TMPDIR=/tmp
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv \
         -d "$OUT/pmc_fetch_$TAG" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu || exit $?
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-        -d "$OUT/pmc_write_$TAG" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu || exit $? ;;
+        -d "$OUT/pmc_write_$TAG" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu || exit $?
+      python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG" 4096 cfg2 \
+        "$OUT/traffic_cfg2_$TAG.json" > /dev/null || exit $? ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
