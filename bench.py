@@ -217,7 +217,7 @@ def main():
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            if tj.get("frames") == F and tj.get("path", "auto") == ("auto" if not args.path else str(args.path)):
+            if tj.get("frames") == F and not args.path and not args.block and not args.warm:
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
