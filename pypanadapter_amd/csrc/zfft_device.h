@@ -1,0 +1,53 @@
+// zfft_device.h -- device helpers shared by the HIP kernel files (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "zfft_internal.h"
+
+namespace zfft {
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2f splat(float a) { return v2f{a, a}; }
+__device__ __forceinline__ v2f vfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ v2f cmul(v2f a, v2f b) {
+  return v2f{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+
+struct IirState {
+  v2f z0[4], z1[4];
+};
+
+__device__ __forceinline__ void state_zero(IirState &s) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s.z0[k] = s.z1[k] = splat(0.f);
+}
+
+__device__ __forceinline__ void state_steady(IirState &s, const Sos32 &c, v2f u0) {
+  // sosfilt_zi(sos) * x0 (sosfiltfilt, _signaltools.py:4817-4824)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    s.z0[k] = c.zi[k][0] * u0;
+    s.z1[k] = c.zi[k][1] * u0;
+  }
+}
+
+// One sample through the 4-section transposed-direct-form-II cascade (scipy _sosfilt).
+// Sections 1..3 have the exact numerator [1, 2, 1]; the gain sits in section 0.
+__device__ __forceinline__ v2f cascade(v2f u, IirState &s, const Sos32 &c) {
+  v2f y = vfma(splat(c.b0), u, s.z0[0]);
+  s.z0[0] = vfma(splat(-c.a1[0]), y, vfma(splat(c.b1), u, s.z1[0]));
+  s.z1[0] = vfma(splat(-c.a2[0]), y, splat(c.b2) * u);
+  u = y;
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    y = u + s.z0[k];
+    s.z0[k] = vfma(splat(-c.a1[k]), y, vfma(splat(2.f), u, s.z1[k]));
+    s.z1[k] = vfma(splat(-c.a2[k]), y, u);
+    u = y;
+  }
+  return u;
+}
+
+}  // namespace zfft

@@ -58,6 +58,21 @@ struct FusedGeom {
 hipError_t launch_fused_pass(const float2 *in, float2 *out, bool desc, bool two, bool nat,
                              const FusedGeom &g, int frames, hipStream_t st);
 
+// Exact-tile decimation stage (xt_kernels.hip): one wave per frame, tiles of 64 lanes x
+// kXtB samples, state scans with the powers of A^kXtB.  Tables computed in fp64 on the host.
+constexpr int kXtB = 16;
+constexpr int kXtT = 64 * kXtB;
+constexpr int kXtScan = 5;          // (A^16)^(2^d), d < 5: (A^16)^32 = A^512 ~ 1e-15 dropped
+constexpr int kXtHeld = kXtB / 2;   // kept (decimated) outputs per lane and tile
+struct XtTables {
+  float M[kXtScan][8][8];     // (A^16)^(2^d), row-major; state order z0_0 z1_0 z0_1 z1_1 ...
+  float Ct[kXtB][8];          // C A^t: output at step t from the entering state
+  float D[64][kXtHeld][8];    // Ct[14 - 2k] (A^16)^(63 - lane): lag correction of kept outputs
+};
+
+hipError_t launch_xt_stage(const float2 *in, int64_t in_stride, int n, const float2 *lo, bool mix,
+                           float2 *out, int frames, const XtTables *tab, hipStream_t st);
+
 struct WelchGeom {
   int n_fft, log2n;
   int n_win;

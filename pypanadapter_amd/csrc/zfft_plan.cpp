@@ -39,6 +39,70 @@ Sos32 sos32() {
 
 namespace {
 
+// ---- exact-tile tables (fp64 -> fp32), state order z0_0 z1_0 z0_1 z1_1 ... ----
+using Mat8 = std::vector<double>;  // 8x8 row-major
+void cascade_d(const double in[8], double u, double out[8], double *y) {
+  double s[8];
+  for (int i = 0; i < 8; ++i) s[i] = in[i];
+  double x = u;
+  for (int k = 0; k < 4; ++k) {
+    const double *c = kDecimSos[k];
+    const double yy = c[0] * x + s[2 * k];
+    s[2 * k] = c[1] * x - c[4] * yy + s[2 * k + 1];
+    s[2 * k + 1] = c[2] * x - c[5] * yy;
+    x = yy;
+  }
+  for (int i = 0; i < 8; ++i) out[i] = s[i];
+  *y = x;
+}
+Mat8 matmul8(const Mat8 &a, const Mat8 &b) {
+  Mat8 c(64, 0.0);
+  for (int i = 0; i < 8; ++i)
+    for (int k = 0; k < 8; ++k)
+      for (int j = 0; j < 8; ++j) c[i * 8 + j] += a[i * 8 + k] * b[k * 8 + j];
+  return c;
+}
+void xt_build_tables(XtTables &T) {
+  Mat8 A(64), I(64, 0.0);
+  double C[8];
+  for (int q = 0; q < 8; ++q) {
+    double e[8] = {0}, s2[8], y;
+    e[q] = 1.0;
+    cascade_d(e, 0.0, s2, &y);
+    for (int r = 0; r < 8; ++r) A[r * 8 + q] = s2[r];
+    C[q] = y;
+    I[q * 8 + q] = 1.0;
+  }
+  Mat8 AB = I;
+  for (int t = 0; t < kXtB; ++t) AB = matmul8(AB, A);
+  Mat8 P = AB;
+  for (int d = 0; d < kXtScan; ++d) {
+    for (int i = 0; i < 64; ++i) T.M[d][i / 8][i % 8] = (float)P[i];
+    P = matmul8(P, P);
+  }
+  std::vector<std::vector<double>> Ct(kXtB, std::vector<double>(8));
+  Mat8 At = I;  // A^t
+  for (int t = 0; t < kXtB; ++t) {
+    for (int q = 0; q < 8; ++q) {
+      double acc = 0;
+      for (int r = 0; r < 8; ++r) acc += C[r] * At[r * 8 + q];
+      Ct[t][q] = acc;
+      T.Ct[t][q] = (float)acc;
+    }
+    At = matmul8(At, A);
+  }
+  Mat8 ABp = I;  // (A^16)^(63 - lane), built from lane 63 downwards
+  for (int lane = 63; lane >= 0; --lane) {
+    for (int k = 0; k < kXtHeld; ++k)
+      for (int q = 0; q < 8; ++q) {
+        double acc = 0;
+        for (int r = 0; r < 8; ++r) acc += Ct[kXtB - 2 - 2 * k][r] * ABp[r * 8 + q];
+        T.D[lane][k][q] = (float)acc;
+      }
+    ABp = matmul8(ABp, AB);
+  }
+}
+
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -100,8 +164,8 @@ struct zfft_plan {
   std::vector<std::string> mark_names;
   std::string names_buf;
   int n_marks = 0;
-  int path = 0;                      // 0 auto, 1 exact pipeline only, 2 fused when applicable
-  DevBuf edge, xk;
+  int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows, 3 exact tiles
+  DevBuf edge, xk, xt_tab;
 };
 
 namespace {
@@ -337,10 +401,32 @@ int run_fused(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
   return ZFFT_OK;
 }
 
+// Exact-tile path: one kernel per stage, one wave per frame, stage outputs natural layout.
+int run_xt(zfft_plan *p, const float2 *d_iq, int64_t L, int frames, const std::vector<int64_t> &n,
+           const float2 **out, hipStream_t st) {
+  hipError_t e = p->ping.ensure((size_t)frames * n[1] * sizeof(float2));
+  if (e == hipSuccess && p->K > 1) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+  const float2 *cur = d_iq;
+  int64_t stride = L;
+  for (int k = 0; k < p->K; ++k) {
+    float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
+    e = launch_xt_stage(cur, stride, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
+                        p->xt_tab.as<XtTables>(), st);
+    if (e != hipSuccess) return hip_fail(e, "xt_stage launch");
+    mark(p, st, k == 0 ? "xt_stage_mix" : "xt_stage");
+    cur = dst;
+    stride = n[k + 1];
+  }
+  *out = cur;
+  return ZFFT_OK;
+}
+
 int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
                   const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   int rc = ensure_lo(p, L);
   if (rc) return rc;
+  if (p->path == 3) return run_xt(p, d_iq, L, frames, n, out, st);
   if (use_fused(p, L)) return run_fused(p, d_iq, L, frames, n, out, st);
   return run_exact(p, d_iq, L, p->lo.as<float2>(), frames, n, out, st);
 }
@@ -474,6 +560,12 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
   e = p->tw.ensure(c.n_fft * sizeof(float2));
   if (e == hipSuccess)
     e = hipMemcpy(p->tw.p, tw.data(), c.n_fft * sizeof(float2), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    XtTables xt;
+    xt_build_tables(xt);
+    e = p->xt_tab.ensure(sizeof(XtTables));
+    if (e == hipSuccess) e = hipMemcpy(p->xt_tab.p, &xt, sizeof(XtTables), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     zfft_plan_destroy(p);
     return hip_fail(e, "twiddle upload");
@@ -487,7 +579,7 @@ int zfft_plan_destroy(zfft_plan *p) {
   (void)hipSetDevice(p->cfg.device);
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->yf, &p->ping, &p->pong, &p->rows,
-                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk})
+                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xt_tab})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -511,7 +603,8 @@ int zfft_plan_timing(zfft_plan *p, int32_t enable) {
 }
 
 int zfft_plan_path(zfft_plan *p, int32_t path) {
-  if (!p || path < 0 || path > 2) return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact) or 2");
+  if (!p || path < 0 || path > 3)
+    return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused) or 3 (exact tiles)");
   p->path = path;
   return ZFFT_OK;
 }

@@ -40,6 +40,19 @@ def test_golden_rows(c):
     assert_row_close(row, golden_rows()[c["name"]], c["name"])
 
 
+@pytest.mark.parametrize("path", [1, 3])
+def test_golden_rows_every_schedule(path):
+    """Every decimator schedule reproduces the reference rows (zoom > 1 cases)."""
+    for c in LDS_CASES:
+        if c["zoom"] == 1:
+            continue
+        x = case_input(c)
+        with _plan_for(c) as plan:
+            plan.set_path(path)
+            row = plan.rows(x)
+        assert_row_close(row, golden_rows()[c["name"]], f"{c['name']} path={path}")
+
+
 def test_zoomfft_fixtures():
     from pypanadapter_amd import ZoomFFT
     zf = np.load(os.path.join(GOLDEN, "zoomfft.npz"))
@@ -156,12 +169,12 @@ def test_fused_interior_matches_exact_pipeline(oracle_lib, N, z, L):
     from pypanadapter_amd import ZoomFFT
     x = _frames(2, L, N, z, N // z, seed0=4200)
     out = {}
-    for path in (1, 2):
+    for path in (1, 2, 3):
         with ZoomFFT(N, z, 2.4e6) as plan:
             plan.set_path(path)
             out[path] = (plan.rows(x), plan.decimate(x[0]))
     ref_dec = oracle_lib.zoomfft(x[0], z, 2.4e6)
-    for path in (1, 2):
+    for path in (1, 2, 3):
         d = out[path][1]
         assert d.shape == ref_dec.shape
         err = np.abs(d - ref_dec) / np.abs(ref_dec).max()
@@ -170,6 +183,7 @@ def test_fused_interior_matches_exact_pipeline(oracle_lib, N, z, L):
         ref = oracle_lib.psd_row(x[f], 2.4e6, N, z, N // z)
         assert_row_close(out[1][0][f], ref, "exact")
         assert_row_close(out[2][0][f], ref, "fused")
+        assert_row_close(out[3][0][f], ref, "exact tiles")
 
 
 def test_size_independent_properties():

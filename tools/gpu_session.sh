@@ -35,7 +35,8 @@ for s in $STEPS; do
       run bench 600 python bench.py --steps 10 --warmup 2 --cpu-seconds 8 || exit $? ;;
     ab)
       run bench_exact 300 python bench.py --steps 5 --warmup 1 --no-cpu --path 1 || exit $?
-      run bench_fused 300 python bench.py --steps 5 --warmup 1 --no-cpu --path 2 || exit $? ;;
+      run bench_fused 300 python bench.py --steps 5 --warmup 1 --no-cpu --path 2 || exit $?
+      run bench_xt 300 python bench.py --steps 5 --warmup 1 --no-cpu --path 3 || exit $? ;;
     sweep)
       for blk in 512 1024 2048 4096; do
         run sweep_b$blk 300 python bench.py --steps 5 --warmup 1 --no-cpu --block $blk || exit $?
