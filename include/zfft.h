@@ -130,6 +130,11 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * the fp32 parity gate; diagnostics / A-B only. */
 int zfft_plan_path(zfft_plan *plan, int32_t path);
 
+/* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 16384, four-step
+ * beyond), 1 = one workgroup per frame (n_fft <= 16384), 2 = four-step N1 x 256 (n_fft in
+ * [4096, 65536]).  Same rows within the parity gate; diagnostics / A-B only. */
+int zfft_plan_welch(zfft_plan *plan, int32_t mode);
+
 const char *zfft_last_error(void);
 int zfft_device_count(void);
 int zfft_version(void);

@@ -54,7 +54,7 @@ EXPORTS = [
     "zfft_decimate", "zfft_decimated_length", "zfft_waterfall_push", "zfft_waterfall_push_device",
     "zfft_waterfall_read", "zfft_waterfall_reset", "zfft_waterfall_shape", "zfft_window_values",
     "zfft_plan_tune", "zfft_plan_timing", "zfft_plan_timings", "zfft_plan_timing_names",
-    "zfft_plan_path", "zfft_last_error",
+    "zfft_plan_path", "zfft_plan_welch", "zfft_last_error",
     "zfft_device_count", "zfft_version",
 ]
 
@@ -114,6 +114,7 @@ def load(path: str = LIB_PATH):
         "zfft_plan_timings": (ctypes.c_int, [P, P, I32, ctypes.POINTER(I32)]),
         "zfft_plan_timing_names": (ctypes.c_char_p, [P]),
         "zfft_plan_path": (ctypes.c_int, [P, I32]),
+        "zfft_plan_welch": (ctypes.c_int, [P, I32]),
         "zfft_last_error": (ctypes.c_char_p, []),
         "zfft_device_count": (ctypes.c_int, []),
         "zfft_version": (ctypes.c_int, []),

@@ -83,6 +83,12 @@ struct WelchGeom {
 hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, const float2 *tw,
                              const WelchGeom &g, float *rows, int frames, hipStream_t st);
 
+// Four-step Welch for N = N1 * 256, 16 <= N1 <= 256: means (frames*nseg), z (frames*nseg*N)
+// workspaces; tws = W_256^m (256) ++ W_N1^m (N1).
+hipError_t launch_welch4(const float2 *x, int64_t len, const float *win, const float2 *tw,
+                         const float2 *tws, const WelchGeom &g, float2 *means, float2 *z,
+                         float *rows, int frames, hipStream_t st);
+
 hipError_t launch_waterfall_init(float *ring, int H, int W, hipStream_t st);
 hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,
                                  int64_t row_stride, int count, int64_t off0, int scroll,

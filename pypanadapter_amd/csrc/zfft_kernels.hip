@@ -647,6 +647,111 @@ __global__ __launch_bounds__(MAXT) void welch_rows_kernel(const v2f *__restrict_
   }
 }
 
+// ------------------------------------------------------------------ Welch row, four-step
+// N = N1 * N2 (N2 = 256) for segments too long for one workgroup's LDS (N = 32768 is in
+// the reference UI's range S:1397, N = 65536 is BASELINE cfg5).  With n = n1 + N1 n2 and
+// k = k2 + N2 k1:  X[k] = sum_n1 W_N1^(n1 k1) W_N^(n1 k2) sum_n2 x[n] W_N2^(n2 k2).
+//   welch4_means: the constant-detrend mean of every segment (one workgroup per segment)
+//   welch4_cols : 16 columns n1 per workgroup (128 B of every row n2 -> coalesced loads);
+//                 mean and window applied on load, length-256 FFT, twiddle W_N^(n1 k2),
+//                 stored as Z[k2][n1] (rows of N1 contiguous samples)
+//   welch4_rows : 16 rows k2 per workgroup, length-N1 FFT per segment, |X|^2 summed over
+//                 the segments in registers, then scale, fftshift crop and 20 log10.
+// tws = [W_256^m, m < 256] ++ [W_N1^m, m < N1].
+__global__ __launch_bounds__(256) void welch4_means_kernel(const v2f *__restrict__ x, int64_t len,
+                                                           WelchGeom g, v2f *__restrict__ means) {
+  __shared__ v2f red[4];
+  const int fs = blockIdx.x;  // frame * nseg + segment
+  const int f = fs / g.nseg, s = fs % g.nseg;
+  const v2f *__restrict__ seg = x + (int64_t)f * len + (int64_t)s * g.step;
+  v2f sum = splat(0.f);
+  for (int n = threadIdx.x; n < g.nperseg; n += 256) sum += seg[n];
+  sum = wave_sum(sum);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    means[fs] = ((red[0] + red[1]) + (red[2] + red[3])) * (1.f / (float)g.nperseg);
+}
+
+constexpr int kN2 = 256;
+constexpr int kColStride = 256 + 16 + 2;  // lp(256) + 2: 16 B aligned, spreads the columns
+
+__global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict__ x, int64_t len,
+                                                          const float *__restrict__ win,
+                                                          const v2f *__restrict__ tw,
+                                                          const v2f *__restrict__ tws, WelchGeom g,
+                                                          const v2f *__restrict__ means,
+                                                          v2f *__restrict__ z) {
+  __shared__ __attribute__((aligned(16))) v2f sh[16 * kColStride];
+  const int N = g.n_fft, N1 = N / kN2, groups = N1 / 16;
+  const int fs = blockIdx.x / groups, cg = blockIdx.x % groups;
+  const int f = fs / g.nseg, s = fs % g.nseg;
+  const int c = threadIdx.x & 15, t = threadIdx.x >> 4;
+  const int n1 = cg * 16 + c;
+  const v2f *__restrict__ seg = x + (int64_t)f * len + (int64_t)s * g.step;
+  const v2f mean = means[fs];
+  v2f v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int n = n1 + N1 * (t + 16 * i);
+    v[i] = n < g.nperseg ? (seg[n] - mean) * win[n] : splat(0.f);  // short branch: zero pad
+  }
+  v2f *col = sh + c * kColStride;
+  stockham_pass<16>(v, t, kN2, 1, tws);
+  stockham_store<16>(v, col, t, kN2, 1);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = col[lp(t + r * 16)];
+  stockham_pass<16>(v, t, kN2, 16, tws);
+  v2f *__restrict__ zs = z + (int64_t)fs * N;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k2 = stockham_out_index<16>(t, kN2, 16, i);
+    zs[(int64_t)k2 * N1 + n1] = cmul(v[i], tw[n1 * k2]);
+  }
+}
+
+template <int R0>
+__global__ __launch_bounds__(256) void welch4_rows_kernel(const v2f *__restrict__ z,
+                                                          const v2f *__restrict__ tws, WelchGeom g,
+                                                          float *__restrict__ rows) {
+  extern __shared__ v2f shr[];
+  const int N = g.n_fft, N1 = N / kN2, T16 = N1 / 16;
+  const int f = blockIdx.x / (kN2 / 16), kg = blockIdx.x % (kN2 / 16);
+  const int c = threadIdx.x / T16, t = threadIdx.x % T16;
+  const int k2 = kg * 16 + c;
+  const v2f *__restrict__ tw1 = tws + kN2;
+  v2f *row_sh = shr + c * (lp(N1) + 2);
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int s = 0; s < g.nseg; ++s) {
+    const v2f *__restrict__ zr = z + ((int64_t)f * g.nseg + s) * N + (int64_t)k2 * N1;
+    v2f v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = zr[t + i * T16];
+    stockham_pass<R0>(v, t, N1, 1, tw1);
+    if (N1 > R0) {
+      stockham_store<R0>(v, row_sh, t, N1, 1);
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = row_sh[lp(t + r * T16)];
+      stockham_pass<16>(v, t, N1, R0, tw1);
+      __syncthreads();  // reads done before the next segment's store
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = fmaf(v[i].x, v[i].x, fmaf(v[i].y, v[i].y, acc[i]));
+  }
+  float *__restrict__ row = rows + (int64_t)f * g.n_win;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k1 = N1 == R0 ? stockham_out_index<R0>(t, N1, 1, i) : stockham_out_index<16>(t, N1, R0, i);
+    const int k = k2 + kN2 * k1;
+    const int j = (k + (g.n_win >> 1)) & (N - 1);  // row[j] = P[(j - W/2) mod N]
+    if (j < g.n_win) row[j] = 20.f * log10f(acc[i] * g.scale);
+  }
+}
+
 // ------------------------------------------------------------------ waterfall ring
 // img[i] == ring[(i + off) mod H]; np.roll(img, -scroll, 0) is off += scroll.
 __global__ void waterfall_init_kernel(float *ring, int H, int W) {
@@ -703,6 +808,12 @@ __global__ void waterfall_read_kernel(const float *__restrict__ ring, int H, int
 
 // ------------------------------------------------------------------ launchers
 static inline unsigned nblocks(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+static inline int ilog2_dev(int v) {
+  int r = 0;
+  while ((1 << (r + 1)) <= v) ++r;
+  return r;
+}
 
 static inline unsigned wave_blocks(const StageGeom &g) {
   return (unsigned)(((int64_t)g.ngroups * g.nblk + 3) / 4);
@@ -799,6 +910,33 @@ hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, con
     case 2: return welch_launch<4>(x, len, win, tw, g, rows, frames, st);
     default: return welch_launch<8>(x, len, win, tw, g, rows, frames, st);
   }
+}
+
+hipError_t launch_welch4(const float2 *x, int64_t len, const float *win, const float2 *tw,
+                         const float2 *tws, const WelchGeom &g, float2 *means, float2 *z,
+                         float *rows, int frames, hipStream_t st) {
+  const int N1 = g.n_fft / kN2;
+  if (N1 < 16 || N1 > 256 || g.n_fft != N1 * kN2) return hipErrorInvalidValue;
+  const unsigned segs = (unsigned)frames * (unsigned)g.nseg;
+  hipLaunchKernelGGL(welch4_means_kernel, dim3(segs), dim3(256), 0, st, (const v2f *)x, len, g,
+                     (v2f *)means);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(welch4_cols_kernel, dim3(segs * (N1 / 16)), dim3(256), 0, st,
+                     (const v2f *)x, len, win, (const v2f *)tw, (const v2f *)tws, g,
+                     (const v2f *)means, (v2f *)z);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t lds = (size_t)16 * (N1 + N1 / 16 + 2) * sizeof(v2f);
+  const dim3 grid((unsigned)frames * (kN2 / 16)), block(N1);
+  const v2f *zc = (const v2f *)z, *tc = (const v2f *)tws;
+  switch (ilog2_dev(N1) % 4) {
+    case 0: hipLaunchKernelGGL(welch4_rows_kernel<16>, grid, block, lds, st, zc, tc, g, rows); break;
+    case 1: hipLaunchKernelGGL(welch4_rows_kernel<2>, grid, block, lds, st, zc, tc, g, rows); break;
+    case 2: hipLaunchKernelGGL(welch4_rows_kernel<4>, grid, block, lds, st, zc, tc, g, rows); break;
+    default: hipLaunchKernelGGL(welch4_rows_kernel<8>, grid, block, lds, st, zc, tc, g, rows); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_waterfall_init(float *ring, int H, int W, hipStream_t st) {

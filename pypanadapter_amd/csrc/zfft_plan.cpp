@@ -165,7 +165,8 @@ struct zfft_plan {
   std::string names_buf;
   int n_marks = 0;
   int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows, 3 exact tiles
-  DevBuf edge, xk, xt_tab;
+  int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
+  DevBuf edge, xk, xt_tab, tws, means, z4;
 };
 
 namespace {
@@ -457,10 +458,21 @@ int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, 
   w.nseg = (int)((Ld - nperseg) / w.step + 1);
   // density scaling 1/(fs*sum(w^2)) and the segment mean (csd average='mean')
   w.scale = (float)(1.0 / (p->cfg.fs * p->win_ss * (double)w.nseg));
-  hipError_t e = launch_welch_rows(x, Ld, p->win.as<float>(), p->tw.as<float2>(), w, d_rows,
-                                   frames, st);
-  if (e != hipSuccess) return hip_fail(e, "welch_rows launch");
-  mark(p, st, "welch_rows");
+  const bool four = p->welch == 2 || (p->welch == 0 && N > kMaxLdsFft);
+  hipError_t e;
+  if (four) {
+    e = p->means.ensure((size_t)frames * w.nseg * sizeof(float2));
+    if (e == hipSuccess) e = p->z4.ensure((size_t)frames * w.nseg * N * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "four-step Welch workspace allocation failed");
+    e = launch_welch4(x, Ld, p->win.as<float>(), p->tw.as<float2>(), p->tws.as<float2>(), w,
+                      p->means.as<float2>(), p->z4.as<float2>(), d_rows, frames, st);
+    if (e != hipSuccess) return hip_fail(e, "welch4 launch");
+    mark(p, st, "welch4");
+  } else {
+    e = launch_welch_rows(x, Ld, p->win.as<float>(), p->tw.as<float2>(), w, d_rows, frames, st);
+    if (e != hipSuccess) return hip_fail(e, "welch_rows launch");
+    mark(p, st, "welch_rows");
+  }
   p->last_row = d_rows + (int64_t)(frames - 1) * p->cfg.n_win;
   return ZFFT_OK;
 }
@@ -520,8 +532,6 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
   const zfft_config &c = *cfg;
   if (!is_pow2(c.n_fft) || c.n_fft < 32 || c.n_fft > 65536)
     return fail(ZFFT_EINVAL, "n_fft must be a power of two in [32, 65536]");
-  if (c.n_fft > kMaxLdsFft)
-    return fail(ZFFT_EUNSUPPORTED, "n_fft > 16384 needs the four-step FFT (not built yet)");
   if (!is_pow2(c.zoom) || c.zoom > 512) return fail(ZFFT_EINVAL, "zoom must be 1, 2, 4, ..., 512");
   if (c.n_win < 2 || c.n_win > c.n_fft || (c.n_win & 1))
     return fail(ZFFT_EINVAL, "n_win must be even and in [2, n_fft]");
@@ -560,6 +570,15 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
   e = p->tw.ensure(c.n_fft * sizeof(float2));
   if (e == hipSuccess)
     e = hipMemcpy(p->tw.p, tw.data(), c.n_fft * sizeof(float2), hipMemcpyHostToDevice);
+  if (e == hipSuccess && c.n_fft >= 4096) {  // four-step sub-FFT twiddles: W_256 ++ W_N1
+    const int n1 = c.n_fft / 256;
+    std::vector<float2> ts(256 + n1);
+    for (int m = 0; m < 256; ++m) ts[m] = tw[(size_t)m * n1];
+    for (int m = 0; m < n1; ++m) ts[256 + m] = tw[(size_t)m * 256];
+    e = p->tws.ensure(ts.size() * sizeof(float2));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->tws.p, ts.data(), ts.size() * sizeof(float2), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) {
     XtTables xt;
     xt_build_tables(xt);
@@ -579,7 +598,8 @@ int zfft_plan_destroy(zfft_plan *p) {
   (void)hipSetDevice(p->cfg.device);
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->yf, &p->ping, &p->pong, &p->rows,
-                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xt_tab})
+                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xt_tab,
+                    &p->tws, &p->means, &p->z4})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -606,6 +626,17 @@ int zfft_plan_path(zfft_plan *p, int32_t path) {
   if (!p || path < 0 || path > 3)
     return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused) or 3 (exact tiles)");
   p->path = path;
+  return ZFFT_OK;
+}
+
+int zfft_plan_welch(zfft_plan *p, int32_t mode) {
+  if (!p || mode < 0 || mode > 2)
+    return fail(ZFFT_EINVAL, "welch mode must be 0 (auto), 1 (one workgroup) or 2 (four-step)");
+  if (mode == 1 && p->cfg.n_fft > kMaxLdsFft)
+    return fail(ZFFT_EUNSUPPORTED, "one-workgroup Welch holds at most 16384 points in LDS");
+  if (mode == 2 && p->cfg.n_fft < 4096)
+    return fail(ZFFT_EINVAL, "four-step Welch needs n_fft >= 4096 (N1 = n_fft/256 >= 16)");
+  p->welch = mode;
   return ZFFT_OK;
 }
 

@@ -95,8 +95,12 @@ class ZoomFFT:
         return [n for n in raw.decode().split(",") if n]
 
     def set_path(self, path: int) -> None:
-        """0 auto, 1 exact reference pass order, 2 fused interior + exact edges."""
+        """0 auto, 1 exact reference pass order, 2 fused interior + exact edges, 3 exact tiles."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
+
+    def set_welch(self, mode: int) -> None:
+        """0 auto, 1 one workgroup per frame (n_fft <= 16384), 2 four-step (n_fft >= 4096)."""
+        check(self.lib.zfft_plan_welch(self._plan, int(mode)), "zfft_plan_welch")
 
     # ---------------------------------------------------------------- DSP
     @staticmethod

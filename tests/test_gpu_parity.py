@@ -13,7 +13,6 @@ from conftest import (GOLDEN, assert_row_close, case_input, golden_cases, golden
 
 pytestmark = pytest.mark.gpu
 CASES = golden_cases()["cases"]
-LDS_CASES = [c for c in CASES if c["n_fft"] <= 16384]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -31,7 +30,7 @@ def _plan_for(c, **kw):
     return ZoomFFT(c["n_fft"], c["zoom"], c["fs"], n_win=c["n_win"], window=w, f_lo=c["f_lo"], **kw)
 
 
-@pytest.mark.parametrize("c", LDS_CASES, ids=[c["name"] for c in LDS_CASES])
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
 def test_golden_rows(c):
     x = case_input(c)
     with _plan_for(c) as plan:
@@ -43,7 +42,7 @@ def test_golden_rows(c):
 @pytest.mark.parametrize("path", [1, 3])
 def test_golden_rows_every_schedule(path):
     """Every decimator schedule reproduces the reference rows (zoom > 1 cases)."""
-    for c in LDS_CASES:
+    for c in CASES:
         if c["zoom"] == 1:
             continue
         x = case_input(c)
@@ -51,6 +50,23 @@ def test_golden_rows_every_schedule(path):
             plan.set_path(path)
             row = plan.rows(x)
         assert_row_close(row, golden_rows()[c["name"]], f"{c['name']} path={path}")
+
+
+def test_golden_rows_four_step_welch():
+    """The four-step Welch (N1 x 256) reproduces the reference rows wherever it applies
+    (n_fft >= 4096), including the short-input branch; the one-workgroup kernel refuses
+    n_fft > 16384 loudly."""
+    big = [c for c in CASES if c["n_fft"] >= 4096]
+    assert any(c["n_fft"] > 16384 for c in big)
+    for c in big:
+        x = case_input(c)
+        with _plan_for(c) as plan:
+            plan.set_welch(2)
+            row = plan.rows(x)
+            if c["n_fft"] > 16384:
+                with pytest.raises(NotImplementedError):
+                    plan.set_welch(1)
+        assert_row_close(row, golden_rows()[c["name"]], f"{c['name']} four-step")
 
 
 def test_zoomfft_fixtures():

@@ -58,8 +58,7 @@ def test_config_validation(zfft_lib, bad):
 
 def test_unsupported_and_nodev(zfft_lib):
     plan = ctypes.c_void_p()
-    rc = zfft_lib.zfft_plan_create(ctypes.byref(_cfg(n_fft=65536, n_win=8192)), None,
-                                   ctypes.byref(plan))
+    rc = zfft_lib.zfft_plan_create(ctypes.byref(_cfg(in_dtype=1)), None, ctypes.byref(plan))
     assert rc == -6
     if zfft_lib.zfft_device_count() == 0:  # CPU container: no GPU -> ENODEV, loudly
         rc = zfft_lib.zfft_plan_create(ctypes.byref(_cfg()), None, ctypes.byref(plan))

@@ -67,6 +67,8 @@ def spectrum_cases():
     add("cfg4_lo150k", 4096, 8, 73, 401, f_lo=1.0 + 150e3)
     add("cfg4_lo-450k", 4096, 8, 73, 402, f_lo=1.0 - 450e3)
     add("cfg5", 65536, 8, 16, 501)
+    add("n32768_z4", 32768, 4, 8, 502)               # largest N of the UI list (S:1397)
+    add("n32768_z64_short", 32768, 64, 8, 503)       # L_d=4096 < N: short-input four-step
     # zoom edge cases
     add("z1_n2048", 2048, 1, 146, 601)
     add("z1_n256_small", 256, 1, 64, 602, store_input=True)
