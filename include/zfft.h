@@ -63,7 +63,7 @@ enum zfft_window_kind {
 };
 
 typedef struct zfft_config {
-  int32_t n_fft;           /* N: power of two, 32..16384 (AppState.fft_size, S:1397)        */
+  int32_t n_fft;           /* N: power of two, 32..65536 (AppState.fft_size, S:1397; cfg5)  */
   int32_t zoom;            /* power of two, 1..512 (AppState.fft_ratio, S:2079-2086)        */
   int32_t n_win;           /* W: row length, even, 2..N (N_WIN S:1757; T:1542)              */
   int32_t window_kind;     /* enum zfft_window_kind                                         */
@@ -71,9 +71,13 @@ typedef struct zfft_config {
   double f_lo;             /* LO frequency, Hz; the reference hard-codes 1.0 (S:2090)       */
   double window_param[2];  /* see window kinds                                              */
   int32_t scroll;          /* waterfall direction, +1 or -1 (AppState.scroll, S:1496)       */
-  int32_t in_dtype;        /* 0 = complex64 (interleaved f32); others reserved              */
+  int32_t in_dtype;        /* 0 = complex64 (interleaved f32, 8 B/sample); 1 = complex32
+                              (interleaved f16, 4 B/sample, BASELINE cfg5); 2 = RTL-SDR
+                              interleaved uint8 I,Q (2 B/sample), value b/127.5 - 1 as
+                              pyrtlsdr's packed_bytes_to_iq                  */
   int32_t device;          /* HIP device ordinal                                            */
-  int32_t flip_input;      /* reserved, must be 0 (np.flip of RTL-SDR sources, S:543)       */
+  int32_t flip_input;      /* 1 = reverse each frame on load: the np.flip the RTL-SDR
+                              sources apply (S:541-543, 459-460), fused into stage 0       */
 } zfft_config;
 
 typedef struct zfft_plan zfft_plan;

@@ -98,9 +98,8 @@ __device__ __forceinline__ void state_scan(IirState &v, const XtTables *__restri
   }
 }
 
-template <bool MIX>
-__global__ __launch_bounds__(256) void xt_stage_kernel(const v2f *__restrict__ in,
-                                                       int64_t in_stride, int n,
+template <bool MIX, int DT>  // DT: input format (stage 0 reads the caller's frames)
+__global__ __launch_bounds__(256) void xt_stage_kernel(InDesc in, int n,
                                                        const v2f *__restrict__ lo,
                                                        v2f *__restrict__ out, int frames,
                                                        const XtTables *__restrict__ tab,
@@ -111,10 +110,9 @@ __global__ __launch_bounds__(256) void xt_stage_kernel(const v2f *__restrict__ i
   if (f >= frames) return;  // whole wave
   v2f *lds = lds_all[wv];
   const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
-  const v2f *__restrict__ x = in + (int64_t)f * in_stride;
   v2f *__restrict__ o = out + (int64_t)f * n_out;
   auto X = [&](int i) -> v2f {
-    v2f v = x[i];
+    v2f v = load_in_t<DT>(in, f, i);
     if constexpr (MIX) v = cmul(v, lo[i]);
     return v;
   };
@@ -253,15 +251,19 @@ __global__ __launch_bounds__(256) void xt_stage_kernel(const v2f *__restrict__ i
   store_kept(nt - 1, held);  // the last tile's top state was exact
 }
 
-hipError_t launch_xt_stage(const float2 *in, int64_t in_stride, int n, const float2 *lo, bool mix,
-                           float2 *out, int frames, const XtTables *tab, hipStream_t st) {
-  const unsigned blocks = (unsigned)((frames + 3) / 4);
-  if (mix)
-    hipLaunchKernelGGL(xt_stage_kernel<true>, dim3(blocks), dim3(256), 0, st, (const v2f *)in,
-                       in_stride, n, (const v2f *)lo, (v2f *)out, frames, tab, sos32());
+hipError_t launch_xt_stage(const InDesc &in, int n, const float2 *lo, bool mix, float2 *out,
+                           int frames, const XtTables *tab, hipStream_t st) {
+  const dim3 grid((unsigned)((frames + 3) / 4)), block(256);
+  const v2f *l = (const v2f *)lo;
+  v2f *o = (v2f *)out;
+  if (!mix)
+    hipLaunchKernelGGL((xt_stage_kernel<false, kInC64>), grid, block, 0, st, in, n, l, o, frames, tab, sos32());
+  else if (in.dtype == kInC64)
+    hipLaunchKernelGGL((xt_stage_kernel<true, kInC64>), grid, block, 0, st, in, n, l, o, frames, tab, sos32());
+  else if (in.dtype == kInC32H)
+    hipLaunchKernelGGL((xt_stage_kernel<true, kInC32H>), grid, block, 0, st, in, n, l, o, frames, tab, sos32());
   else
-    hipLaunchKernelGGL(xt_stage_kernel<false>, dim3(blocks), dim3(256), 0, st, (const v2f *)in,
-                       in_stride, n, (const v2f *)lo, (v2f *)out, frames, tab, sos32());
+    hipLaunchKernelGGL((xt_stage_kernel<true, kInCU8>), grid, block, 0, st, in, n, l, o, frames, tab, sos32());
   return hipGetLastError();
 }
 

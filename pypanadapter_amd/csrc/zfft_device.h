@@ -15,6 +15,30 @@ __device__ __forceinline__ v2f cmul(v2f a, v2f b) {
   return v2f{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
 }
 
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef unsigned char u8x2 __attribute__((ext_vector_type(2)));
+
+// Sample index i of frame f of the caller's input as complex64 (InDesc, zfft_internal.h).
+template <int DT>
+__device__ __forceinline__ v2f load_in_t(const InDesc &d, int64_t f, int64_t i) {
+  const int64_t k = f * d.stride + (d.flip ? d.len - 1 - i : i);
+  if constexpr (DT == kInC64) {
+    return ((const v2f *)d.p)[k];
+  } else if constexpr (DT == kInC32H) {
+    const h2 h = ((const h2 *)d.p)[k];
+    return v2f{(float)h.x, (float)h.y};
+  } else {
+    const u8x2 b = ((const u8x2 *)d.p)[k];
+    return v2f{((float)b.x - 127.5f) * (1.f / 127.5f), ((float)b.y - 127.5f) * (1.f / 127.5f)};
+  }
+}
+
+__device__ __forceinline__ v2f load_in(const InDesc &d, int64_t f, int64_t i) {
+  if (d.dtype == kInC64) return load_in_t<kInC64>(d, f, i);
+  if (d.dtype == kInC32H) return load_in_t<kInC32H>(d, f, i);
+  return load_in_t<kInCU8>(d, f, i);
+}
+
 struct IirState {
   v2f z0[4], z1[4];
 };

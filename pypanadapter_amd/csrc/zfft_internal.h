@@ -23,6 +23,19 @@ struct Sos32 {
 
 Sos32 sos32();
 
+// The caller's frames (the `chunk` of S:2102 / T:1516): sample i of frame f is element
+// f * stride + (flip ? len - 1 - i : i) of p, in one of the zfft_config in_dtype formats:
+//   0 complex64 (interleaved f32), 1 complex32 (interleaved f16, BASELINE cfg5),
+//   2 RTL-SDR interleaved uint8 I,Q, value b/127.5 - 1 (pyrtlsdr packed_bytes_to_iq).
+// flip fuses the sources' np.flip (S:541-543, 459-460) into the stage-0 loads.
+enum InDtype { kInC64 = 0, kInC32H = 1, kInCU8 = 2 };
+struct InDesc {
+  const void *p;
+  int64_t stride, len;
+  int dtype, flip;
+};
+inline size_t in_elem_bytes(int dtype) { return dtype == kInC64 ? 8 : dtype == kInC32H ? 4 : 2; }
+
 // --- kernels (zfft_kernels.hip); all enqueue on `st`, return hipError_t of the launch ---
 // Intermediates use the frame-group-interleaved (FGI) layout: element (f, j) of a
 // per-frame sequence of length len lives at ((f/64)*len + j)*64 + f%64 (float2 units);
@@ -37,7 +50,7 @@ struct StageGeom {
   int64_t alt_off = 0;   // ... starting alt_off samples into each frame (edge windows)
 };
 
-hipError_t launch_iir_forward_mix(const float2 *in, int64_t L, int frames, const float2 *lo,
+hipError_t launch_iir_forward_mix(const InDesc &in, int frames, const float2 *lo,
                                   float2 *yf, const StageGeom &g, hipStream_t st);
 hipError_t launch_iir_forward_fgi(const float2 *in, float2 *yf, const StageGeom &g,
                                   hipStream_t st);
@@ -70,7 +83,7 @@ struct XtTables {
   float D[64][kXtHeld][8];    // Ct[14 - 2k] (A^16)^(63 - lane): lag correction of kept outputs
 };
 
-hipError_t launch_xt_stage(const float2 *in, int64_t in_stride, int n, const float2 *lo, bool mix,
+hipError_t launch_xt_stage(const InDesc &in, int n, const float2 *lo, bool mix,
                            float2 *out, int frames, const XtTables *tab, hipStream_t st);
 
 struct WelchGeom {
@@ -95,8 +108,9 @@ hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,
                                  hipStream_t st);
 hipError_t launch_waterfall_read(const float *ring, int H, int W, int64_t off, float *img,
                                  hipStream_t st);
-hipError_t launch_mix(const float2 *in, const float2 *lo, float2 *out, int64_t n,
-                      hipStream_t st);
+// out[f][i] = in(f, i) (* lo[i] when lo) as complex64, natural layout, frames x len.
+hipError_t launch_ingest(const InDesc &in, const float2 *lo, float2 *out, int frames,
+                         hipStream_t st);
 
 // --- host helpers ---
 void set_error(const std::string &msg);

@@ -154,8 +154,8 @@ __global__ __launch_bounds__(256) void iir_forward_fgi_kernel(const v2f *__restr
 constexpr int kTile = 16;
 constexpr int kTileStride = kTile + 2;  // float2 units: 144 B rows, 16 B aligned, conflict-free
 
-__global__ __launch_bounds__(256) void iir_forward_mix_kernel(const v2f *__restrict__ in,
-                                                              int64_t L, int frames,
+template <int DT>
+__global__ __launch_bounds__(256) void iir_forward_mix_kernel(InDesc in, int frames,
                                                               const v2f *__restrict__ lo,
                                                               v2f *__restrict__ yf, StageGeom g,
                                                               Sos32 c) {
@@ -168,14 +168,14 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(const v2f *__restr
   // Frame groups at or above g.split (a multiple of 64, 0 = none) are a second set of
   // windows starting g.alt_off samples into the same frames (edge windows, one launch).
   const bool second = g.split > 0 && w.fg * 64 >= g.split;
-  const v2f *__restrict__ inb = in + (second ? g.alt_off : 0);
-  const v2f *__restrict__ lob = lo + (second ? g.alt_off : 0);
+  const int64_t o = second ? g.alt_off : 0;  // window start in the frame
+  const v2f *__restrict__ lob = lo + o;
   const int f0 = w.fg * 64 - (second ? g.split : 0);  // frame index of row 0 in its set
   // loader geometry: element (row r = 4q + lane/16, col k = lane%16)
   const int lrow = w.lane >> 4, lcol = w.lane & 15;
 
-  auto xm = [&](int f, int i) -> v2f {  // mixed sample of frame f at index i (natural layout)
-    return cmul(inb[(int64_t)f * L + i], lob[i]);
+  auto xm = [&](int f, int i) -> v2f {  // mixed sample i of the window of frame f
+    return cmul(load_in_t<DT>(in, f, o + i), lob[i]);
   };
   auto ext_slow = [&](int f, int j) -> v2f {
     if (f >= frames || j < 0 || j >= e) return splat(0.f);
@@ -190,9 +190,8 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(const v2f *__restr
     const bool fast = jc >= kPad && jc + kTile <= n + kPad && f0 + 64 <= frames;  // uniform
     if (fast) {
       const v2f l = lob[j - kPad];
-      const v2f *p = inb + (int64_t)(f0 + lrow) * L + (j - kPad);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) pf[q] = cmul(p[(int64_t)q * 4 * L], l);
+      for (int q = 0; q < 16; ++q) pf[q] = cmul(load_in_t<DT>(in, f0 + lrow + 4 * q, o + j - kPad), l);
     } else {
 #pragma unroll
       for (int q = 0; q < 16; ++q) pf[q] = ext_slow(f0 + 4 * q + lrow, j);
@@ -405,11 +404,16 @@ __global__ __launch_bounds__(256) void fused_pass_kernel(const v2f *__restrict__
   for (; q < count; ++q) step(q, IN(DESC ? j_first - q : j_first + q));
 }
 
-__global__ __launch_bounds__(256) void mix_kernel(const v2f *__restrict__ in,
-                                                  const v2f *__restrict__ lo,
-                                                  v2f *__restrict__ out, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = cmul(in[i], lo[i]);
+// The caller's frames as complex64, mixed with the LO when lo != nullptr (zoom 1 paths and
+// zoomfft(x, 1), S:2093-2094).
+template <int DT>
+__global__ __launch_bounds__(256) void ingest_kernel(InDesc in, const v2f *__restrict__ lo,
+                                                     v2f *__restrict__ out, int64_t total) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= total) return;
+  const int64_t f = k / in.len, i = k - f * in.len;
+  const v2f v = load_in_t<DT>(in, f, i);
+  out[k] = lo ? cmul(v, lo[i]) : v;
 }
 
 // ------------------------------------------------------------------ Welch row
@@ -819,10 +823,17 @@ static inline unsigned wave_blocks(const StageGeom &g) {
   return (unsigned)(((int64_t)g.ngroups * g.nblk + 3) / 4);
 }
 
-hipError_t launch_iir_forward_mix(const float2 *in, int64_t L, int frames, const float2 *lo,
-                                  float2 *yf, const StageGeom &g, hipStream_t st) {
-  hipLaunchKernelGGL(iir_forward_mix_kernel, dim3(wave_blocks(g)), dim3(256), 0, st,
-                     (const v2f *)in, L, frames, (const v2f *)lo, (v2f *)yf, g, sos32());
+hipError_t launch_iir_forward_mix(const InDesc &in, int frames, const float2 *lo, float2 *yf,
+                                  const StageGeom &g, hipStream_t st) {
+  const dim3 grid(wave_blocks(g)), block(256);
+  const v2f *l = (const v2f *)lo;
+  v2f *y = (v2f *)yf;
+  if (in.dtype == kInC64)
+    hipLaunchKernelGGL(iir_forward_mix_kernel<kInC64>, grid, block, 0, st, in, frames, l, y, g, sos32());
+  else if (in.dtype == kInC32H)
+    hipLaunchKernelGGL(iir_forward_mix_kernel<kInC32H>, grid, block, 0, st, in, frames, l, y, g, sos32());
+  else
+    hipLaunchKernelGGL(iir_forward_mix_kernel<kInCU8>, grid, block, 0, st, in, frames, l, y, g, sos32());
   return hipGetLastError();
 }
 
@@ -865,10 +876,18 @@ hipError_t launch_fused_pass(const float2 *in, float2 *out, bool desc, bool two,
   return hipGetLastError();
 }
 
-hipError_t launch_mix(const float2 *in, const float2 *lo, float2 *out, int64_t n,
-                      hipStream_t st) {
-  hipLaunchKernelGGL(mix_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, (const v2f *)in,
-                     (const v2f *)lo, (v2f *)out, n);
+hipError_t launch_ingest(const InDesc &in, const float2 *lo, float2 *out, int frames,
+                         hipStream_t st) {
+  const int64_t total = (int64_t)frames * in.len;
+  const dim3 grid(nblocks(total, 256)), block(256);
+  const v2f *l = (const v2f *)lo;
+  v2f *o = (v2f *)out;
+  if (in.dtype == kInC64)
+    hipLaunchKernelGGL(ingest_kernel<kInC64>, grid, block, 0, st, in, l, o, total);
+  else if (in.dtype == kInC32H)
+    hipLaunchKernelGGL(ingest_kernel<kInC32H>, grid, block, 0, st, in, l, o, total);
+  else
+    hipLaunchKernelGGL(ingest_kernel<kInCU8>, grid, block, 0, st, in, l, o, total);
   return hipGetLastError();
 }
 

@@ -267,7 +267,7 @@ int check_lengths(const zfft_plan *p, int64_t L, int32_t frames, std::vector<int
 // stage) in natural layout in *out.
 // With split > 0 (a multiple of 64) the frames [split, split + frames) are a second window
 // set starting alt_off samples into the same frames; the output then has split + frames rows.
-int run_exact(zfft_plan *p, const float2 *in, int64_t stride, const float2 *lo, int frames,
+int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
               const std::vector<int64_t> &n, const float2 **out, hipStream_t st, int split = 0,
               int64_t alt_off = 0) {
   const int rows = split > 0 ? split + frames : frames;
@@ -277,7 +277,7 @@ int run_exact(zfft_plan *p, const float2 *in, int64_t stride, const float2 *lo, 
   if (e == hipSuccess) e = p->ping.ensure(G * n[1] * sizeof(float2));
   if (e == hipSuccess && p->K > 1) e = p->pong.ensure(G * n[2] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
-  const float2 *cur = in;
+  const float2 *cur = nullptr;
   for (int k = 0; k < p->K; ++k) {
     StageGeom g;
     g.n = (int)n[k];
@@ -288,7 +288,7 @@ int run_exact(zfft_plan *p, const float2 *in, int64_t stride, const float2 *lo, 
     g.split = split;
     g.alt_off = alt_off;
     if (k == 0)
-      e = launch_iir_forward_mix(in, stride, frames, lo, p->yf.as<float2>(), g, st);
+      e = launch_iir_forward_mix(in, frames, lo, p->yf.as<float2>(), g, st);
     else
       e = launch_iir_forward_fgi(cur, p->yf.as<float2>(), g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
@@ -322,7 +322,7 @@ int fused_block(int64_t n_mid, int ngroups) {
 //   [C0] [A0 A1] [C1 C2] [A2 A3] ... [last pass of stage K-1, decimated, natural layout]
 // then the first/last kEdge outputs are replaced by the exact pipeline on prefix/suffix
 // windows of the frames (run first, their edge outputs parked in p->edge).
-int run_fused(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
+int run_fused(zfft_plan *p, const InDesc &in, int64_t L, int frames,
               const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   const int K = p->K;
   const int64_t nK = n[K];
@@ -345,7 +345,7 @@ int run_fused(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
   // [nsuf_K - E, nsuf_K) -> p->edge [F][2E]
   const int Fp = ngroups * 64;
   const float2 *w;
-  int rc = run_exact(p, d_iq, L, p->lo.as<float2>(), frames, npre, &w, st, Fp, L0);
+  int rc = run_exact(p, in, p->lo.as<float2>(), frames, npre, &w, st, Fp, L0);
   if (rc) return rc;
   e = hipMemcpy2DAsync(edge, 2 * kEdge * sizeof(float2), w, npre[K] * sizeof(float2),
                        kEdge * sizeof(float2), frames, hipMemcpyDeviceToDevice, st);
@@ -363,7 +363,7 @@ int run_fused(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
   g0.nblk = (int)((L + kPad + g0.block - 1) / g0.block);
   g0.warmup = warmup(p);
   g0.ngroups = ngroups;
-  e = launch_iir_forward_mix(d_iq, L, frames, p->lo.as<float2>(), p->yf.as<float2>(), g0, st);
+  e = launch_iir_forward_mix(in, frames, p->lo.as<float2>(), p->yf.as<float2>(), g0, st);
   if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
   mark(p, st, "C0_forward_mix");
   const float2 *cur = p->yf.as<float2>();
@@ -403,36 +403,39 @@ int run_fused(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
 }
 
 // Exact-tile path: one kernel per stage, one wave per frame, stage outputs natural layout.
-int run_xt(zfft_plan *p, const float2 *d_iq, int64_t L, int frames, const std::vector<int64_t> &n,
+int run_xt(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t> &n,
            const float2 **out, hipStream_t st) {
   hipError_t e = p->ping.ensure((size_t)frames * n[1] * sizeof(float2));
   if (e == hipSuccess && p->K > 1) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
-  const float2 *cur = d_iq;
-  int64_t stride = L;
+  const float2 *cur = nullptr;
   for (int k = 0; k < p->K; ++k) {
     float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
-    e = launch_xt_stage(cur, stride, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
+    const InDesc src = k == 0 ? in : InDesc{cur, n[k], n[k], kInC64, 0};
+    e = launch_xt_stage(src, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
                         p->xt_tab.as<XtTables>(), st);
     if (e != hipSuccess) return hip_fail(e, "xt_stage launch");
     mark(p, st, k == 0 ? "xt_stage_mix" : "xt_stage");
     cur = dst;
-    stride = n[k + 1];
   }
   *out = cur;
   return ZFFT_OK;
 }
 
-int run_decimator(zfft_plan *p, const float2 *d_iq, int64_t L, int frames,
+int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
                   const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   int rc = ensure_lo(p, L);
   if (rc) return rc;
-  if (p->path == 3) return run_xt(p, d_iq, L, frames, n, out, st);
-  if (use_fused(p, L)) return run_fused(p, d_iq, L, frames, n, out, st);
-  return run_exact(p, d_iq, L, p->lo.as<float2>(), frames, n, out, st);
+  if (p->path == 3) return run_xt(p, in, frames, n, out, st);
+  if (use_fused(p, L)) return run_fused(p, in, L, frames, n, out, st);
+  return run_exact(p, in, p->lo.as<float2>(), frames, n, out, st);
 }
 
-int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, float *d_rows,
+InDesc input_of(const zfft_plan *p, const void *d_iq, int64_t L) {
+  return InDesc{d_iq, L, L, p->cfg.in_dtype, p->cfg.flip_input};
+}
+
+int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, float *d_rows,
                    hipStream_t st) {
   std::vector<int64_t> n;
   int rc = check_lengths(p, L, frames, n);
@@ -442,12 +445,20 @@ int process_device(zfft_plan *p, const float2 *d_iq, int64_t L, int32_t frames, 
   const int nperseg = (int)(Ld < N ? Ld : N);
   rc = ensure_window(p, nperseg);
   if (rc) return rc;
-  const float2 *x = d_iq;
+  const InDesc in = input_of(p, d_iq, L);
+  const float2 *x = (const float2 *)d_iq;
   p->n_marks = 0;
   mark(p, st, "start");
   if (p->K > 0) {
-    rc = run_decimator(p, d_iq, L, frames, n, &x, st);
+    rc = run_decimator(p, in, L, frames, n, &x, st);
     if (rc) return rc;
+  } else if (in.dtype != kInC64 || in.flip) {  // zoom 1: Welch reads complex64 frames
+    hipError_t e = p->dec.ensure((size_t)frames * L * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "ingest workspace allocation failed");
+    e = launch_ingest(in, nullptr, p->dec.as<float2>(), frames, st);
+    if (e != hipSuccess) return hip_fail(e, "ingest launch");
+    mark(p, st, "ingest");
+    x = p->dec.as<float2>();
   }
   WelchGeom w;
   w.n_fft = N;
@@ -538,8 +549,9 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
   if (!(c.fs > 0) || !std::isfinite(c.fs) || !std::isfinite(c.f_lo))
     return fail(ZFFT_EINVAL, "fs must be positive and finite, f_lo finite");
   if (c.scroll != 1 && c.scroll != -1) return fail(ZFFT_EINVAL, "scroll must be +1 or -1");
-  if (c.in_dtype != 0) return fail(ZFFT_EUNSUPPORTED, "only complex64 input (in_dtype 0)");
-  if (c.flip_input != 0) return fail(ZFFT_EUNSUPPORTED, "flip_input is not built yet");
+  if (c.in_dtype < kInC64 || c.in_dtype > kInCU8)
+    return fail(ZFFT_EINVAL, "in_dtype must be 0 (complex64), 1 (complex32 f16) or 2 (RTL-SDR u8)");
+  if (c.flip_input != 0 && c.flip_input != 1) return fail(ZFFT_EINVAL, "flip_input must be 0 or 1");
   if (c.window_kind == ZFFT_WIN_ARRAY) {
     if (!window_or_null) return fail(ZFFT_EINVAL, "ZFFT_WIN_ARRAY needs a window array");
   } else if (!window_kind_native(c.window_kind)) {
@@ -675,7 +687,7 @@ int zfft_process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frame
   int rc = enter(p);
   if (rc) return rc;
   if (!d_iq || !d_rows) return fail(ZFFT_EINVAL, "null device pointer");
-  return process_device(p, (const float2 *)d_iq, L, frames, d_rows, pick_stream(p, hip_stream));
+  return process_device(p, d_iq, L, frames, d_rows, pick_stream(p, hip_stream));
 }
 
 int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float *rows_out) {
@@ -683,14 +695,14 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
   if (rc) return rc;
   if (!iq || !rows_out) return fail(ZFFT_EINVAL, "null host pointer");
   if (L < 1 || frames < 1) return fail(ZFFT_EINVAL, "n_samples and n_frames must be >= 1");
-  const size_t in_bytes = (size_t)frames * L * sizeof(float2);
+  const size_t in_bytes = (size_t)frames * L * in_elem_bytes(p->cfg.in_dtype);
   const size_t row_bytes = (size_t)frames * p->cfg.n_win * sizeof(float);
   hipError_t e = p->in.ensure(in_bytes);
   if (e == hipSuccess) e = p->rows.ensure(row_bytes);
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "staging allocation failed");
   e = hipMemcpyAsync(p->in.p, iq, in_bytes, hipMemcpyHostToDevice, p->stream);
   if (e != hipSuccess) return hip_fail(e, "H2D copy");
-  rc = process_device(p, p->in.as<float2>(), L, frames, p->rows.as<float>(), p->stream);
+  rc = process_device(p, p->in.p, L, frames, p->rows.as<float>(), p->stream);
   if (rc) return rc;
   e = hipMemcpyAsync(rows_out, p->rows.p, row_bytes, hipMemcpyDeviceToHost, p->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
@@ -705,9 +717,10 @@ int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t
   std::vector<int64_t> n;
   rc = check_lengths(p, L, 1, n);
   if (rc) return rc;
-  hipError_t e = p->in.ensure((size_t)L * sizeof(float2));
+  const size_t in_bytes = (size_t)L * in_elem_bytes(p->cfg.in_dtype);
+  hipError_t e = p->in.ensure(in_bytes);
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "staging allocation failed");
-  e = hipMemcpyAsync(p->in.p, iq, (size_t)L * sizeof(float2), hipMemcpyHostToDevice, p->stream);
+  e = hipMemcpyAsync(p->in.p, iq, in_bytes, hipMemcpyHostToDevice, p->stream);
   if (e != hipSuccess) return hip_fail(e, "H2D copy");
   const float2 *x;
   if (p->K == 0) {  // zoomfft(x, 1) still mixes (S:2093-2094)
@@ -715,11 +728,12 @@ int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t
     if (rc) return rc;
     e = p->dec.ensure((size_t)L * sizeof(float2));
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "allocation failed");
-    e = launch_mix(p->in.as<float2>(), p->lo.as<float2>(), p->dec.as<float2>(), L, p->stream);
+    e = launch_ingest(input_of(p, p->in.p, L), p->lo.as<float2>(), p->dec.as<float2>(), 1,
+                      p->stream);
     if (e != hipSuccess) return hip_fail(e, "mix launch");
     x = p->dec.as<float2>();
   } else {
-    rc = run_decimator(p, p->in.as<float2>(), L, 1, n, &x, p->stream);
+    rc = run_decimator(p, input_of(p, p->in.p, L), L, 1, n, &x, p->stream);
     if (rc) return rc;
   }
   const int64_t m = n[p->K];

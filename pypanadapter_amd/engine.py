@@ -33,12 +33,23 @@ def _window_spec(window):
     return _lib.WINDOW_KINDS[name], (p[0], p[1]), None
 
 
+# in_dtype name -> (zfft_config.in_dtype, numpy element type of the host array)
+IN_DTYPES = {"complex64": (0, np.complex64), "complex32": (1, np.float16), "cu8": (2, np.uint8)}
+
+
 class ZoomFFT:
     """A plan: IQ frames -> dB rows (+ the on-device waterfall ring)."""
 
     def __init__(self, n_fft: int, zoom: int, fs: float, n_win: int | None = None,
-                 window="hamming", f_lo: float = 1.0, scroll: int = 1, device: int = 0):
+                 window="hamming", f_lo: float = 1.0, scroll: int = 1, device: int = 0,
+                 in_dtype: str = "complex64", flip: bool = False):
+        """in_dtype: "complex64" (complex ndarray), "complex32" (float16 interleaved I,Q,
+        shape (..., 2L)) or "cu8" (RTL-SDR uint8 interleaved I,Q, value b/127.5 - 1).
+        flip: reverse every frame on load (the sources' np.flip, S:541-543)."""
         self.lib = _lib.load()
+        if in_dtype not in IN_DTYPES:
+            raise ValueError(f"in_dtype must be one of {sorted(IN_DTYPES)}")
+        self.in_dtype, self.flip = in_dtype, bool(flip)
         self.n_fft, self.zoom, self.fs, self.f_lo = int(n_fft), int(zoom), float(fs), float(f_lo)
         self.n_win = int(n_win) if n_win is not None else self.n_fft // self.zoom
         kind, params, arr = _window_spec(window)
@@ -46,7 +57,8 @@ class ZoomFFT:
         cfg.n_fft, cfg.zoom, cfg.n_win, cfg.window_kind = self.n_fft, self.zoom, self.n_win, kind
         cfg.fs, cfg.f_lo = self.fs, self.f_lo
         cfg.window_param[0], cfg.window_param[1] = params
-        cfg.scroll, cfg.in_dtype, cfg.device, cfg.flip_input = int(scroll), 0, int(device), 0
+        cfg.scroll, cfg.device = int(scroll), int(device)
+        cfg.in_dtype, cfg.flip_input = IN_DTYPES[in_dtype][0], int(self.flip)
         if arr is not None and arr.size != self.n_fft:
             raise ValueError("array window must have length n_fft (welch nperseg)")
         self._window_array = arr  # kept alive for the call
@@ -103,19 +115,28 @@ class ZoomFFT:
         check(self.lib.zfft_plan_welch(self._plan, int(mode)), "zfft_plan_welch")
 
     # ---------------------------------------------------------------- DSP
-    @staticmethod
-    def _as_iq(x) -> np.ndarray:
+    def _as_iq(self, x) -> np.ndarray:
+        """The caller's frames in the plan's input format, C-contiguous; the last axis holds
+        L complex samples (complex64) or 2L interleaved I,Q values (complex32, cu8)."""
         x = np.asarray(x)
-        if x.dtype != np.complex64:
-            x = x.astype(np.complex64)
+        dt = IN_DTYPES[self.in_dtype][1]
+        if self.in_dtype == "complex64":
+            if x.dtype != dt:
+                x = x.astype(dt)
+        elif x.dtype != dt or x.shape[-1] % 2:
+            raise ValueError(f"{self.in_dtype} input must be {np.dtype(dt).name} with "
+                             "interleaved I,Q on the last axis")
         return np.ascontiguousarray(x)
+
+    def _samples(self, x) -> int:
+        return x.shape[-1] if self.in_dtype == "complex64" else x.shape[-1] // 2
 
     def rows(self, frames) -> np.ndarray:
         """(F, L) or (L,) complex IQ -> (F, W) or (W,) float32 dB rows."""
         x = self._as_iq(frames)
         single = x.ndim == 1
         x2 = x.reshape(1, -1) if single else x
-        F, L = x2.shape
+        F, L = x2.shape[0], self._samples(x2)
         out = np.empty((F, self.n_win), dtype=np.float32)
         check(self.lib.zfft_process(self._plan, x2.ctypes.data_as(ctypes.c_void_p), L, F,
                                     out.ctypes.data_as(ctypes.c_void_p)), "zfft_process")
@@ -131,10 +152,11 @@ class ZoomFFT:
     def decimate(self, x) -> np.ndarray:
         """zoomfft(x, zoom) of the reference (S:2088-2100) -> complex64."""
         x = self._as_iq(x).ravel()
-        m = self.lib.zfft_decimated_length(len(x), self.zoom)
+        L = self._samples(x)
+        m = self.lib.zfft_decimated_length(L, self.zoom)
         out = np.empty(max(m, 1), dtype=np.complex64)
         n_out = ctypes.c_int64()
-        check(self.lib.zfft_decimate(self._plan, x.ctypes.data_as(ctypes.c_void_p), len(x),
+        check(self.lib.zfft_decimate(self._plan, x.ctypes.data_as(ctypes.c_void_p), L,
                                      out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n_out)),
               "zfft_decimate")
         return out[:n_out.value]

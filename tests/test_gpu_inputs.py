@@ -1,0 +1,99 @@
+"""GPU parity of the caller-input formats fused into the stage-0 loads (zfft_config in_dtype,
+flip_input): complex64, complex32 (f16, BASELINE cfg5) and RTL-SDR uint8,
+each optionally reversed per frame (the sources' np.flip, S:541-543 / 459-460).
+
+The oracle sees the same values the kernel is handed: the fp16 input widened to complex64
+exactly, the uint8 bytes normalised as pyrtlsdr's packed_bytes_to_iq does (b/127.5 - 1, fp64;
+pyrtlsdr is not vendored in the reference, so that normalisation is "parity unpinned" beyond
+its published formula), and np.flip applied per frame.  Gate as every other row test."""
+import numpy as np
+import pytest
+
+from conftest import assert_row_close, case_input, golden_cases, golden_rows, row_errors
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(F, L, N, z, W, seed0):
+    from pypanadapter_amd import synth
+    return np.stack([synth.make_iq(L, 2.4e6, seed0 + f, n_fft=N, zoom=z, n_win=W)
+                     for f in range(F)])
+
+
+def _encode(x, fmt):
+    """complex64 frames -> (array handed to the engine, complex128 values it represents)."""
+    if fmt == "complex64":
+        return x, x.astype(np.complex128)
+    if fmt == "complex32":
+        h = np.ascontiguousarray(x).view(np.float32).astype(np.float16)
+        v = h.astype(np.float64)
+        return h, v[..., 0::2] + 1j * v[..., 1::2]
+    # cu8: an 8-bit ADC view of the same signal (RTL-SDR read_bytes layout I,Q,I,Q,...)
+    iq = np.ascontiguousarray(x).view(np.float32).astype(np.float64)
+    b = np.clip(np.rint(127.5 + 127.5 * 0.25 * iq), 0, 255).astype(np.uint8)
+    v = b.astype(np.float64) / 127.5 - 1.0
+    return b, v[..., 0::2] + 1j * v[..., 1::2]
+
+
+CONFIGS = [(1024, 8, 65536, 3), (4096, 8, 299008, 2), (2048, 2, 100003, 2), (256, 1, 16411, 3)]
+
+
+@pytest.mark.parametrize("fmt", ["complex64", "complex32", "cu8"])
+@pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
+@pytest.mark.parametrize("N,z,L,F", CONFIGS, ids=[f"N{c[0]}_z{c[1]}_L{c[2]}" for c in CONFIGS])
+def test_input_format_rows_vs_oracle(oracle_lib, fmt, flip, N, z, L, F):
+    from pypanadapter_amd import ZoomFFT
+    W = N // z
+    x = _frames(F, L, N, z, W, seed0=2000 + N + z)
+    arr, vals = _encode(x, fmt)
+    ref_in = vals[:, ::-1] if flip else vals
+    refs = [oracle_lib.psd_row(ref_in[f], 2.4e6, N, z, W) for f in range(F)]
+    for path in ([0, 1, 3] if z > 1 else [0]):
+        with ZoomFFT(N, z, 2.4e6, n_win=W, in_dtype=fmt, flip=flip) as plan:
+            plan.set_path(path)
+            rows = plan.rows(arr)
+        for f in range(F):
+            assert_row_close(rows[f], refs[f], f"{fmt} flip={flip} path={path} frame {f}")
+
+
+@pytest.mark.parametrize("fmt", ["complex32", "cu8"])
+def test_input_format_decimate(oracle_lib, fmt):
+    """zoomfft(x, ratio) on the converted input (S:2088-2100), including ratio 1 (mix only)."""
+    from pypanadapter_amd import ZoomFFT
+    x = _frames(1, 40000, 1024, 4, 256, seed0=2500)[0]
+    arr, vals = _encode(x, fmt)
+    for ratio in (1, 4):
+        with ZoomFFT(1024, ratio, 2.4e6, in_dtype=fmt, flip=True) as plan:
+            y = plan.decimate(arr)
+        ref = oracle_lib.zoomfft(vals[::-1], ratio, 2.4e6)
+        err = np.abs(y - ref).max() / np.abs(ref).max()
+        assert err < 2e-6, (fmt, ratio, err)
+
+
+def test_cfg5_fp16_storage_gate():
+    """BASELINE cfg5: frames stored as complex32 against the reference's fp32/fp64 rows, under
+    SURVEY §8c's fp16-storage gate (|ddB| <= 0.05 within 40 dB of peak, |d amp| <= 1e-3 x
+    peak); fp32 arithmetic throughout."""
+    from pypanadapter_amd import ZoomFFT
+    c = next(c for c in golden_cases()["cases"] if c["name"] == "cfg5")
+    x = case_input(c)
+    h, _ = _encode(x, "complex32")
+    with ZoomFFT(c["n_fft"], c["zoom"], c["fs"], n_win=c["n_win"], in_dtype="complex32") as plan:
+        row = plan.rows(h)
+    ref = golden_rows()["cfg5"].astype(np.float64)
+    pk = ref.max()
+    m = ref > pk - 40.0
+    assert np.abs(row - ref)[m].max() <= 0.05
+    _, damp = row_errors(row, ref)
+    assert damp <= 1e-3
+
+
+def test_input_format_rejects_wrong_arrays():
+    from pypanadapter_amd import ZoomFFT
+    with ZoomFFT(1024, 4, 2.4e6, in_dtype="cu8") as plan:
+        with pytest.raises(ValueError):
+            plan.rows(np.zeros(4096, np.float16))
+        with pytest.raises(ValueError):
+            plan.rows(np.zeros(4097, np.uint8))
+    with pytest.raises(ValueError):
+        ZoomFFT(1024, 4, 2.4e6, in_dtype="complex128")
