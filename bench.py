@@ -39,7 +39,14 @@ CONFIGS = {
                  desc="N_FFT=16384 with 50%-overlap Welch averaging, fp32, 1 MI355X"),
     "cfg1": dict(n_fft=1024, zoom=4, fs=2.4e6, n_avg=256, frames=4096,
                  desc="256k-sample frames, N_FFT=1024, zoom=4"),
+    "cfg4": dict(n_fft=4096, zoom=8, fs=2.4e6, n_avg=73, frames=4096, lo_step=150e3,
+                 desc="8 independent IF centre frequencies (f_LO = 1 Hz + rank*150 kHz), one "
+                      "stream per GPU"),
+    "cfg5": dict(n_fft=65536, zoom=8, fs=2.4e6, n_avg=16, frames=512,
+                 desc="1M-sample frames, N_FFT=65536, four-step Welch; --in-dtype complex32 "
+                      "for fp16 IQ storage"),
 }
+IN_BYTES = {"complex64": 8, "complex32": 4, "cu8": 2}
 TONES = ((0.31, 1.0), (-0.57, 0.1))
 
 
@@ -124,6 +131,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--in-dtype", default="complex64", choices=sorted(IN_BYTES),
+                    help="IQ storage format in HBM (cfg5: complex32 = fp16)")
     args = ap.parse_args()
 
     cfg = dict(CONFIGS[args.config])
@@ -149,7 +158,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from pypanadapter_amd import ZoomFFT
-    plan = ZoomFFT(N, zoom, fs, n_win=W, device=local)
+    f_lo = 1.0 + cfg.get("lo_step", 0.0) * rank
+    plan = ZoomFFT(N, zoom, fs, n_win=W, device=local, f_lo=f_lo, in_dtype=args.in_dtype)
     if args.block or args.warm:
         plan.tune(args.block, args.warm)
     if args.path:
@@ -158,6 +168,10 @@ def main():
     torch.cuda.set_stream(stream)    # read by the C-ABI as "the plan's own stream"
     sp = stream.cuda_stream
     x = make_frames(torch, F, L, cfg, dev, 1234 + rank)
+    if args.in_dtype == "complex32":
+        x = x.to(torch.float16).contiguous()
+    elif args.in_dtype == "cu8":
+        x = torch.clamp(torch.round(127.5 + 127.5 * 0.25 * x), 0, 255).to(torch.uint8).contiguous()
     rows = torch.empty((F, W), dtype=torch.float32, device=dev)
     torch.cuda.synchronize(dev)
 
@@ -204,7 +218,8 @@ def main():
     total_samples = F * L * args.steps * world
     value = total_samples / wall_max / 1e6
     lines = F * args.steps * world / wall_max
-    alg_bytes_step = F * (8 * L + 8 * W)  # 8*L in + 4*W row + 4*W ring row
+    bps = IN_BYTES[args.in_dtype]
+    alg_bytes_step = F * (bps * L + 8 * W)  # bps*L in + 4*W row + 4*W ring row
     ev_ms_step = ev_max / args.steps * 1e3
     achieved = alg_bytes_step / (ev_ms_step / 1e3) / 1e9
     names = plan.launch_names()
@@ -217,7 +232,8 @@ def main():
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            if tj.get("frames") == F and not args.path and not args.block and not args.warm:
+            if (tj.get("frames") == F and tj.get("in_dtype", "complex64") == args.in_dtype
+                    and not args.path and not args.block and not args.warm):
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
@@ -232,11 +248,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if args.in_dtype == "complex64" else f"f32 ({args.in_dtype} IQ storage)",
         "data": "synthetic (device-generated complex white noise + 2 in-band tones, seed per rank)",
         "config": {"workload": f"{args.config}: {cfg['desc']}", "n_fft": N, "zoom": zoom,
                    "n_win": W, "samples_per_line": L, "frames_per_rank": F, "fs": fs,
-                   "window": "hamming", "parallelism": f"frame-sharded x{world}, no collective"},
+                   "window": "hamming", "in_dtype": args.in_dtype, "f_lo_rank0": 1.0,
+                   "parallelism": f"frame-sharded x{world}, no collective"},
         "lines_per_s": round(lines, 1),
         "roofline": {"bound": "hbm", "kernel": "IQ->log-PSD path (all launches of one step)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

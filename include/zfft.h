@@ -128,7 +128,8 @@ int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *coun
 /* Comma-separated names of the intervals zfft_plan_timings returns (owned by the plan). */
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
-/* Decimator schedule: 0 = automatic, 1 = blocked warm-up passes in the reference order,
+/* Decimator schedule: 0 = automatic (3 for batches of >= 256 frames, else 2 where the frame
+ * is long enough for its edge windows, else 1), 1 = blocked warm-up passes in the reference order,
  * 2 = fused commuted-order interior + exact edge windows, 3 = exact tiles (one wave per
  * frame, state scans, no intermediate in memory).  All produce the reference's rows within
  * the fp32 parity gate; diagnostics / A-B only. */

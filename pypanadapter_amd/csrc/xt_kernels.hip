@@ -7,103 +7,123 @@
 //
 // A wave walks its frame in tiles of 1024 samples; lane i owns the 16-sample sub-block i.
 //  forward (exact):  every lane runs the cascade from a zero state over its sub-block;
-//                    a Kogge-Stone scan over the 64 lane end-states with the matrices
-//                    (A^16)^(2^d) gives each lane its true entering state (the tile's
-//                    entering state folded into lane 0), and the outputs are corrected
-//                    by C A^t s_in.  The scan stops at d = 4: (A^16)^32 = A^512 ~ 1e-15.
+//                    its end state goes to the real modal basis of A (T^-1, block lower
+//                    triangular), where a sub-block step is one complex multiply per
+//                    mode; a Kogge-Stone scan over the lanes, per mode only as deep as its
+//                    pole radius needs (.587 .682 .808 .935 -> 2 2 3 5 levels,
+//                    |lambda|^(16*2^L) < 1e-9), gives each lane its entering state (the
+//                    tile's entering state folded into lane 0), and the outputs are
+//                    corrected by C A^t T m_in.
 //  backward:         the same over the forward outputs in descending order, with the
 //                    state entering the tile from above provisionally zero.  The state
-//                    this leaves at the tile bottom is exact anyway (its dependence on
-//                    the unknown top state is A^1024 ~ 1e-30), and it is precisely the
-//                    top state of the tile below, which was processed one step earlier:
-//                    its kept outputs get the correction D[lane][k] . q (table), then
-//                    are stored.  One tile of lag.
+//                    this leaves at the tile bottom is exact anyway (its dependence on the
+//                    top state is lambda^1024 < 1e-29), and it is precisely the top state
+//                    of the tile below, which was processed one step earlier: its kept
+//                    outputs get C A^(15-t) T lambda^(16 (63-lane)) q, then are stored.
 //  frame ends:       forward starts from zi * ext[0]; the last tile's backward starts from
 //                    zi * y[e-1] with a constant y[e-1] tail above e-1 (the steady state
 //                    is a fixed point of the recursion), exactly scipy's initial condition.
-// Numerics: float32, max relative error vs float64 sosfiltfilt ~7.6e-7 on white noise,
-// the same as a sequential float32 sosfiltfilt (6.2e-7): /tmp-free reproduction in
-// tools/xt_proto.py.
+// Numerics: float32; tools/xt_modal_proto.py models the schedule (fp32 max relative error
+// vs float64 sosfiltfilt 9.5e-7 on white noise; plain float32 sosfiltfilt 5.8e-7).
 #include "zfft_device.h"
 
 namespace zfft {
 
-constexpr int kXtLdsStride = kXtB + 1;  // padded sub-block rows: conflict-free ds_read_b64
+constexpr int kXtLdsStride = kXtB + 1;      // padded sub-block rows: conflict-free ds_read_b64
+constexpr int kLevels[4] = {2, 2, 3, kXtScan};
+
+struct Modal {
+  v2f r[8];  // a0 b0 a1 b1 a2 b2 a3 b3 (complex: I and Q of the frame share the real basis)
+};
 
 __device__ __forceinline__ v2f sget(const IirState &s, int r) {
   return (r & 1) ? s.z1[r >> 1] : s.z0[r >> 1];
 }
-__device__ __forceinline__ void sset(IirState &s, int r, v2f v) {
-  if (r & 1) s.z1[r >> 1] = v;
-  else s.z0[r >> 1] = v;
-}
 
-__device__ __forceinline__ v2f shfl2(v2f v, int src) {
-  return v2f{__shfl(v.x, src, 64), __shfl(v.y, src, 64)};
-}
-
-// a wave-uniform value into scalar registers (every lane holds the same state)
 __device__ __forceinline__ float uni(float a) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(a)));
 }
 __device__ __forceinline__ v2f uni2(v2f v) { return v2f{uni(v.x), uni(v.y)}; }
-
-// uniform state = state of lane `src` (broadcast, kept in SGPRs)
-__device__ __forceinline__ void bcast_state(const IirState &v, int src, IirState &out) {
-#pragma unroll
-  for (int r = 0; r < 8; ++r) sset(out, r, uni2(shfl2(sget(v, r), src)));
+__device__ __forceinline__ v2f lane_of(v2f v, int src) {  // value of lane src, uniform
+  return v2f{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), src)),
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), src))};
+}
+__device__ __forceinline__ v2f shfl2(v2f v, int src) {
+  return v2f{__shfl(v.x, src, 64), __shfl(v.y, src, 64)};
 }
 
-// Compiler-only barrier: the table constants below are re-read (scalar loads, K$ hits)
-// after it instead of being hoisted out of the tile loop into ~900 SGPRs.
-__device__ __forceinline__ void refetch_tables() { asm volatile("" ::: "memory"); }
+// The table pointer laundered through an opaque (volatile) asm: loads through the result
+// stay scalar (K$ hits) but cannot be hoisted above it, so each phase of the tile loop
+// re-reads the few constants it needs instead of the compiler keeping every table entry
+// live across the loop in SGPRs (and spilling them).
+// Constant address space (AS4): reads of uniform addresses are s_load (the table is never
+// written by a kernel), and the pointer keeps that property through the asm.
+typedef const XtModal __attribute__((address_space(4))) *CTab;
+__device__ __forceinline__ CTab fresh(CTab p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
 
-// out = M s (8x8 real matrix, row-major, uniform) applied to both channels
-__device__ __forceinline__ void matvec(const float *__restrict__ M, const IirState &s,
-                                       IirState &out) {
+// (a, b) <- [[c, s], [-s, c]] (a, b): one mode times lambda^p = c + i s
+__device__ __forceinline__ void rot(v2f &a, v2f &b, float c, float s) {
+  const v2f na = vfma(splat(c), a, splat(s) * b);
+  b = vfma(splat(c), b, splat(-s) * a);
+  a = na;
+}
+
+// m = T^-1 z; T^-1 is block lower triangular (mode j depends on sections <= j)
+__device__ __forceinline__ void to_modal(CTab tab, const IirState &z,
+                                         Modal &m) {
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    refetch_tables();
+    CTab tb = fresh(tab);
     v2f acc = splat(0.f);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc = vfma(splat(M[r * 8 + q]), sget(s, q), acc);
-    sset(out, r, acc);
+    for (int q = 0; q < (r | 1) + 1; ++q) acc = vfma(splat(tb->ti[r][q]), sget(z, q), acc);
+    m.r[r] = acc;
   }
 }
 
-// inclusive Kogge-Stone scan of lane states in the direction UP (lane i accumulates lanes
-// j <= i) or down (j >= i): v_i = sum_j (A^16)^|i-j| z_j.
+__device__ __forceinline__ v2f dot_cm(CTab tab, int t, const Modal &m,
+                                      v2f acc) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) acc = vfma(splat(tab->cm[t][r]), m.r[r], acc);
+  return acc;
+}
+
+// inclusive scan over lanes: UP (lane i accumulates lanes j <= i) or down (j >= i),
+// m_i = sum_j lambda^(16 |i-j|) m_j per mode
 template <bool UP>
-__device__ __forceinline__ void state_scan(IirState &v, const XtTables *__restrict__ tab, int lane) {
-#pragma unroll 1
-  for (int d = 0; d < kXtScan; ++d) {
-    const int sh = 1 << d;
-    const int src = UP ? lane - sh : lane + sh;
-    const bool take = UP ? lane >= sh : lane + sh <= 63;
-    IirState w;
+__device__ __forceinline__ void modal_scan(Modal &m, CTab tab, int lane) {
+  // an opaque copy of the lane id: the per-level masks and shuffle addresses below are
+  // recomputed here (a few VALU ops) rather than hoisted into the loop preheader, where
+  // they would pin ~20 SGPR pairs and VGPRs for the whole kernel
+  asm volatile("" : "+v"(lane));
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const v2f t = shfl2(sget(v, r), src & 63);
-      sset(w, r, take ? t : splat(0.f));
-    }
-    const float *__restrict__ M = &tab->M[d][0][0];
+  for (int j = 0; j < 4; ++j) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      refetch_tables();  // one row of constants live at a time
-      v2f acc = sget(v, r);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc = vfma(splat(M[r * 8 + q]), sget(w, q), acc);
-      sset(v, r, acc);
+    for (int d = 0; d < kLevels[j]; ++d) {
+      const int sh = 1 << d;
+      const bool take = UP ? lane >= sh : lane + sh <= 63;
+      const int src = (UP ? lane - sh : lane + sh) & 63;
+      v2f pa = shfl2(m.r[2 * j], src), pb = shfl2(m.r[2 * j + 1], src);
+      pa = take ? pa : splat(0.f);
+      pb = take ? pb : splat(0.f);
+      CTab tb = fresh(tab);
+      rot(pa, pb, tb->scan[d][j][0], tb->scan[d][j][1]);
+      m.r[2 * j] += pa;
+      m.r[2 * j + 1] += pb;
     }
   }
 }
 
-template <bool MIX, int DT>  // DT: input format (stage 0 reads the caller's frames)
-__global__ __launch_bounds__(256) void xt_stage_kernel(InDesc in, int n,
+template <bool MIX, int DT, int FLIP>  // DT, FLIP: input format (stage 0 reads the caller's frames)
+__global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
                                                        const v2f *__restrict__ lo,
                                                        v2f *__restrict__ out, int frames,
-                                                       const XtTables *__restrict__ tab,
+                                                       const XtModal *tab_g,
                                                        Sos32 c) {
+  const CTab tab = (CTab)tab_g;
   __shared__ __attribute__((aligned(16))) v2f lds_all[4][64 * kXtLdsStride];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int f = blockIdx.x * 4 + wv;
@@ -112,7 +132,7 @@ __global__ __launch_bounds__(256) void xt_stage_kernel(InDesc in, int n,
   const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
   v2f *__restrict__ o = out + (int64_t)f * n_out;
   auto X = [&](int i) -> v2f {
-    v2f v = load_in_t<DT>(in, f, i);
+    v2f v = load_in_t<DT, FLIP>(in, f, i);
     if constexpr (MIX) v = cmul(v, lo[i]);
     return v;
   };
@@ -124,8 +144,19 @@ __global__ __launch_bounds__(256) void xt_stage_kernel(InDesc in, int n,
   };
   const int nt = (e + kXtT - 1) / kXtT;
 
-  IirState s_in;  // state entering the current tile (forward), wave-uniform (SGPRs)
-  state_steady(s_in, c, uni2(ext(0)));
+  // per-lane powers lambda^(16 (63 - lane)): the held tile's lanes from its top state
+  float lgc[4], lgs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lgc[j] = tab->lag[63 - lane][j][0];
+    lgs[j] = tab->lag[63 - lane][j][1];
+  }
+  Modal m_in;  // modal state entering the current tile (forward), wave-uniform
+  {
+    const v2f x0 = uni2(ext(0));
+#pragma unroll
+    for (int r = 0; r < 8; ++r) m_in.r[r] = uni2(tab->zim[r] * x0);
+  }
   v2f held[kXtHeld];  // previous tile's kept backward outputs, awaiting the lag correction
 
   auto store_kept = [&](int tile, const v2f *val) {  // decimated outputs -> frame row
@@ -147,102 +178,110 @@ __global__ __launch_bounds__(256) void xt_stage_kernel(InDesc in, int n,
     const int base = tau * kXtT;
     // ---- tile -> LDS (coalesced: 64 consecutive samples per load instruction) ----
     const bool fast = base >= kPad && base + kXtT <= n + kPad;  // wave-uniform
+    // sample s = lane + 64 q -> row s/16 = lane/16 + 4 q, column lane%16
+    v2f *st = lds + (lane >> 4) * kXtLdsStride + (lane & 15);
+    if (fast) {
 #pragma unroll
-    for (int q = 0; q < kXtB; ++q) {
-      const int s = lane + 64 * q;
-      lds[(s >> 4) * kXtLdsStride + (s & 15)] = fast ? X(base + s - kPad) : ext(base + s);
+      for (int q = 0; q < kXtB; ++q) st[4 * kXtLdsStride * q] = X(base - kPad + lane + 64 * q);
+    } else {
+#pragma unroll
+      for (int q = 0; q < kXtB; ++q) st[4 * kXtLdsStride * q] = ext(base + lane + 64 * q);
     }
     __builtin_amdgcn_wave_barrier();
     v2f y[kXtB];
+    const v2f *row = lds + lane * kXtLdsStride;
 #pragma unroll
-    for (int t = 0; t < kXtB; ++t) y[t] = lds[lane * kXtLdsStride + t];
+    for (int t = 0; t < kXtB; ++t) y[t] = row[t];
     __builtin_amdgcn_wave_barrier();
 
     // ---- forward pass ----
-    IirState v;
-    state_zero(v);
-#pragma unroll
-    for (int t = 0; t < kXtB; ++t) y[t] = cascade(y[t], v, c);
+    Modal m;
     {
-      refetch_tables();
-      IirState u;
-      matvec(&tab->M[0][0][0], s_in, u);  // lane 0 also carries (A^16) s_in
+      IirState v;
+      state_zero(v);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) sset(v, r, sget(v, r) + (lane == 0 ? sget(u, r) : splat(0.f)));
+      for (int t = 0; t < kXtB; ++t) y[t] = cascade(y[t], v, c);
+      to_modal(tab, v, m);
     }
-    state_scan<true>(v, tab, lane);
-    IirState se;  // state entering this lane's sub-block
+    {  // lane 0 also carries lambda^16 m_in (the tile's entering state)
+      CTab tb = fresh(tab);
+      Modal u = m_in;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const v2f up = shfl2(sget(v, r), (lane + 63) & 63);
-      sset(se, r, lane == 0 ? sget(s_in, r) : up);
+      for (int j = 0; j < 4; ++j) rot(u.r[2 * j], u.r[2 * j + 1], tb->p16[j][0], tb->p16[j][1]);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) m.r[r] += lane == 0 ? u.r[r] : splat(0.f);
     }
-    bcast_state(v, 63, s_in);  // next tile's entering state
+    modal_scan<true>(m, tab, lane);
+    {
+      Modal me;  // state entering this lane's sub-block
 #pragma unroll
-    for (int t = 0; t < kXtB; ++t) {
-      refetch_tables();
-      v2f acc = y[t];
+      for (int r = 0; r < 8; ++r) {
+        const v2f up = shfl2(m.r[r], (lane + 63) & 63);
+        me.r[r] = lane == 0 ? m_in.r[r] : up;
+      }
 #pragma unroll
-      for (int r = 0; r < 8; ++r) acc = vfma(splat(tab->Ct[t][r]), sget(se, r), acc);
-      y[t] = acc;
+      for (int r = 0; r < 8; ++r) m_in.r[r] = lane_of(m.r[r], 63);  // next tile's entering state
+#pragma unroll
+      for (int t = 0; t < kXtB; ++t) y[t] = dot_cm(fresh(tab), t, me, y[t]);
     }
 
     // ---- backward pass ----
     const bool last = tau == nt - 1;
-    IirState qtop;
-    state_zero(qtop);
+    v2f ylast = splat(0.f);
     if (last) {  // steady state zi * y[e-1] above the frame end, constant tail
       const int pl = e - 1 - base;
-      v2f cand = y[0];
+      v2f *w = lds + lane * kXtLdsStride;
 #pragma unroll
-      for (int t = 1; t < kXtB; ++t)
-        if (t == (pl & 15)) cand = y[t];
-      const v2f ylast = uni2(shfl2(cand, pl >> 4));
+      for (int t = 0; t < kXtB; ++t) w[t] = y[t];
+      __builtin_amdgcn_wave_barrier();
+      ylast = uni2(lds[(pl >> 4) * kXtLdsStride + (pl & 15)]);
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int t = 0; t < kXtB; ++t)
         if (base + lane * kXtB + t >= e) y[t] = ylast;
-      state_steady(qtop, c, ylast);
     }
-    state_zero(v);
     v2f kept[kXtHeld];
+    {
+      IirState v;
+      state_zero(v);
 #pragma unroll
-    for (int t = kXtB - 1; t >= 0; --t) {
-      const v2f yb = cascade(y[t], v, c);
-      if (t & 1) kept[t >> 1] = yb;  // j = base + 16 lane + t odd <=> (j - 27) even
+      for (int t = kXtB - 1; t >= 0; --t) {
+        const v2f yb = cascade(y[t], v, c);
+        if (t & 1) kept[t >> 1] = yb;  // j = base + 16 lane + t odd <=> (j - 27) even
+      }
+      to_modal(tab, v, m);
     }
+    Modal qtop;  // state entering the tile from above: exact steady state on the last tile
+#pragma unroll
+    for (int r = 0; r < 8; ++r) qtop.r[r] = last ? fresh(tab)->zim[r] * ylast : splat(0.f);
     if (last) {
-      refetch_tables();
-      IirState u;
-      matvec(&tab->M[0][0][0], qtop, u);
+      CTab tb = fresh(tab);
+      Modal u = qtop;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) sset(v, r, sget(v, r) + (lane == 63 ? sget(u, r) : splat(0.f)));
+      for (int j = 0; j < 4; ++j) rot(u.r[2 * j], u.r[2 * j + 1], tb->p16[j][0], tb->p16[j][1]);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) m.r[r] += lane == 63 ? u.r[r] : splat(0.f);
     }
-    state_scan<false>(v, tab, lane);
-    IirState qe;  // state entering this lane's sub-block from above
+    modal_scan<false>(m, tab, lane);
+    {
+      Modal qe;  // state entering this lane's sub-block from above
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const v2f dn = shfl2(sget(v, r), (lane + 1) & 63);
-      sset(qe, r, lane == 63 ? sget(qtop, r) : dn);
-    }
+      for (int r = 0; r < 8; ++r) {
+        const v2f dn = shfl2(m.r[r], (lane + 1) & 63);
+        qe.r[r] = lane == 63 ? qtop.r[r] : dn;
+      }
 #pragma unroll
-    for (int k = 0; k < kXtHeld; ++k) {
-      refetch_tables();
-      v2f acc = kept[k];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) acc = vfma(splat(tab->Ct[kXtB - 2 - 2 * k][r]), sget(qe, r), acc);
-      kept[k] = acc;
+      for (int k = 0; k < kXtHeld; ++k) kept[k] = dot_cm(fresh(tab), kXtB - 2 - 2 * k, qe, kept[k]);
     }
     // ---- the tile below is now complete: its top state is this tile's bottom state ----
     if (tau > 0) {
-      IirState qb;
-      bcast_state(v, 0, qb);
+      Modal q;
 #pragma unroll
-      for (int k = 0; k < kXtHeld; ++k) {
-        v2f acc = held[k];
+      for (int r = 0; r < 8; ++r) q.r[r] = lane_of(m.r[r], 0);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) acc = vfma(splat(tab->D[lane][k][r]), sget(qb, r), acc);
-        held[k] = acc;
-      }
+      for (int j = 0; j < 4; ++j) rot(q.r[2 * j], q.r[2 * j + 1], lgc[j], lgs[j]);
+#pragma unroll
+      for (int k = 0; k < kXtHeld; ++k) held[k] = dot_cm(fresh(tab), kXtB - 2 - 2 * k, q, held[k]);
       store_kept(tau - 1, held);
     }
 #pragma unroll
@@ -251,19 +290,28 @@ __global__ __launch_bounds__(256) void xt_stage_kernel(InDesc in, int n,
   store_kept(nt - 1, held);  // the last tile's top state was exact
 }
 
+template <bool MIX, int DT, int FLIP>
+static void xt_launch(const InDesc &in, int n, const float2 *lo, float2 *out, int frames,
+                      const XtModal *tab, hipStream_t st) {
+  hipLaunchKernelGGL((xt_stage_kernel<MIX, DT, FLIP>), dim3((unsigned)((frames + 3) / 4)), dim3(256),
+                     0, st, in, n, (const v2f *)lo, (v2f *)out, frames, tab, sos32());
+}
+
 hipError_t launch_xt_stage(const InDesc &in, int n, const float2 *lo, bool mix, float2 *out,
-                           int frames, const XtTables *tab, hipStream_t st) {
-  const dim3 grid((unsigned)((frames + 3) / 4)), block(256);
-  const v2f *l = (const v2f *)lo;
-  v2f *o = (v2f *)out;
-  if (!mix)
-    hipLaunchKernelGGL((xt_stage_kernel<false, kInC64>), grid, block, 0, st, in, n, l, o, frames, tab, sos32());
-  else if (in.dtype == kInC64)
-    hipLaunchKernelGGL((xt_stage_kernel<true, kInC64>), grid, block, 0, st, in, n, l, o, frames, tab, sos32());
-  else if (in.dtype == kInC32H)
-    hipLaunchKernelGGL((xt_stage_kernel<true, kInC32H>), grid, block, 0, st, in, n, l, o, frames, tab, sos32());
-  else
-    hipLaunchKernelGGL((xt_stage_kernel<true, kInCU8>), grid, block, 0, st, in, n, l, o, frames, tab, sos32());
+                           int frames, const XtModal *tab, hipStream_t st) {
+  if (!mix) {
+    if (in.dtype != kInC64 || in.flip) return hipErrorInvalidValue;  // stages >= 1: internal
+    xt_launch<false, kInC64, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInC64) {
+    if (in.flip) xt_launch<true, kInC64, 1>(in, n, lo, out, frames, tab, st);
+    else xt_launch<true, kInC64, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInC32H) {
+    if (in.flip) xt_launch<true, kInC32H, 1>(in, n, lo, out, frames, tab, st);
+    else xt_launch<true, kInC32H, 0>(in, n, lo, out, frames, tab, st);
+  } else {
+    if (in.flip) xt_launch<true, kInCU8, 1>(in, n, lo, out, frames, tab, st);
+    else xt_launch<true, kInCU8, 0>(in, n, lo, out, frames, tab, st);
+  }
   return hipGetLastError();
 }
 

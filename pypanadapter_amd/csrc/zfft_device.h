@@ -19,9 +19,11 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef unsigned char u8x2 __attribute__((ext_vector_type(2)));
 
 // Sample index i of frame f of the caller's input as complex64 (InDesc, zfft_internal.h).
-template <int DT>
+// FLIP: -1 = read d.flip at run time, 0 / 1 = known at compile time (immediate offsets).
+template <int DT, int FLIP = -1>
 __device__ __forceinline__ v2f load_in_t(const InDesc &d, int64_t f, int64_t i) {
-  const int64_t k = f * d.stride + (d.flip ? d.len - 1 - i : i);
+  const bool flip = FLIP < 0 ? d.flip != 0 : FLIP != 0;
+  const int64_t k = f * d.stride + (flip ? d.len - 1 - i : i);
   if constexpr (DT == kInC64) {
     return ((const v2f *)d.p)[k];
   } else if constexpr (DT == kInC32H) {

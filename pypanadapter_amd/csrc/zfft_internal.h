@@ -72,19 +72,23 @@ hipError_t launch_fused_pass(const float2 *in, float2 *out, bool desc, bool two,
                              const FusedGeom &g, int frames, hipStream_t st);
 
 // Exact-tile decimation stage (xt_kernels.hip): one wave per frame, tiles of 64 lanes x
-// kXtB samples, state scans with the powers of A^kXtB.  Tables computed in fp64 on the host.
+// kXtB samples, lane states scanned in the real modal basis of the cascade's state matrix
+// A (4 rotation-scaling modes, one per section pole pair).  fp64 on the host -> fp32.
 constexpr int kXtB = 16;
 constexpr int kXtT = 64 * kXtB;
-constexpr int kXtScan = 5;          // (A^16)^(2^d), d < 5: (A^16)^32 = A^512 ~ 1e-15 dropped
+constexpr int kXtScan = 5;          // scan levels of the slowest mode (radius 0.9351)
 constexpr int kXtHeld = kXtB / 2;   // kept (decimated) outputs per lane and tile
-struct XtTables {
-  float M[kXtScan][8][8];     // (A^16)^(2^d), row-major; state order z0_0 z1_0 z0_1 z1_1 ...
-  float Ct[kXtB][8];          // C A^t: output at step t from the entering state
-  float D[64][kXtHeld][8];    // Ct[14 - 2k] (A^16)^(63 - lane): lag correction of kept outputs
+struct XtModal {
+  float ti[8][8];          // T^-1: DF2T state (z0_0 z1_0 z0_1 ...) -> modal (a0 b0 a1 b1 ...)
+  float zim[8];            // T^-1 zi: steady state per unit input (sosfilt_zi)
+  float cm[kXtB][8];       // C A^t T: output t samples after a modal state
+  float p16[4][2];         // lambda_j^16 (re, im): one lane sub-block
+  float scan[kXtScan][4][2];  // lambda_j^(16 * 2^d): scan level d
+  float lag[64][4][2];     // lambda_j^(16 i): i sub-blocks down from the tile top
 };
 
 hipError_t launch_xt_stage(const InDesc &in, int n, const float2 *lo, bool mix,
-                           float2 *out, int frames, const XtTables *tab, hipStream_t st);
+                           float2 *out, int frames, const XtModal *tab, hipStream_t st);
 
 struct WelchGeom {
   int n_fft, log2n;

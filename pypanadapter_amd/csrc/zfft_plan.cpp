@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <complex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -62,8 +63,44 @@ Mat8 matmul8(const Mat8 &a, const Mat8 &b) {
       for (int j = 0; j < 8; ++j) c[i * 8 + j] += a[i * 8 + k] * b[k * 8 + j];
   return c;
 }
-void xt_build_tables(XtTables &T) {
-  Mat8 A(64), I(64, 0.0);
+// Real modal basis of the cascade's state matrix A (block lower triangular: section k's
+// state is driven by the outputs of sections < k).  Mode j = the pole pair of section j,
+// lambda_j = sigma + i omega = (-a1 + i sqrt(4 a2 - a1^2)) / 2; its eigenvector v is zero on
+// sections < j, the null vector of (A_jj - lambda) on section j and found by forward
+// substitution below.  Columns (Re v, Im v) of T give T^-1 A T = diag([[sigma, omega],
+// [-omega, sigma]]), so a power of A is a per-mode complex power (tools/xt_modal_proto.py).
+using cd = std::complex<double>;
+
+void mat_inverse8(const Mat8 &a, Mat8 &inv) {
+  Mat8 m = a;
+  inv.assign(64, 0.0);
+  for (int i = 0; i < 8; ++i) inv[i * 8 + i] = 1.0;
+  for (int c = 0; c < 8; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < 8; ++r)
+      if (std::fabs(m[r * 8 + c]) > std::fabs(m[piv * 8 + c])) piv = r;
+    for (int k = 0; k < 8; ++k) {
+      std::swap(m[c * 8 + k], m[piv * 8 + k]);
+      std::swap(inv[c * 8 + k], inv[piv * 8 + k]);
+    }
+    const double d = m[c * 8 + c];
+    for (int k = 0; k < 8; ++k) {
+      m[c * 8 + k] /= d;
+      inv[c * 8 + k] /= d;
+    }
+    for (int r = 0; r < 8; ++r) {
+      if (r == c) continue;
+      const double f = m[r * 8 + c];
+      for (int k = 0; k < 8; ++k) {
+        m[r * 8 + k] -= f * m[c * 8 + k];
+        inv[r * 8 + k] -= f * inv[c * 8 + k];
+      }
+    }
+  }
+}
+
+void xt_build_tables(XtModal &X) {
+  Mat8 A(64);
   double C[8];
   for (int q = 0; q < 8; ++q) {
     double e[8] = {0}, s2[8], y;
@@ -71,35 +108,72 @@ void xt_build_tables(XtTables &T) {
     cascade_d(e, 0.0, s2, &y);
     for (int r = 0; r < 8; ++r) A[r * 8 + q] = s2[r];
     C[q] = y;
-    I[q * 8 + q] = 1.0;
   }
-  Mat8 AB = I;
-  for (int t = 0; t < kXtB; ++t) AB = matmul8(AB, A);
-  Mat8 P = AB;
-  for (int d = 0; d < kXtScan; ++d) {
-    for (int i = 0; i < 64; ++i) T.M[d][i / 8][i % 8] = (float)P[i];
-    P = matmul8(P, P);
+  Mat8 T(64, 0.0);
+  cd lam[4];
+  for (int j = 0; j < 4; ++j) {
+    const double a1 = kDecimSos[j][4], a2 = kDecimSos[j][5];
+    lam[j] = cd(-0.5 * a1, std::sqrt(a2 - 0.25 * a1 * a1));
+    cd v[8] = {};
+    const double p = A[(2 * j) * 8 + 2 * j], q = A[(2 * j) * 8 + 2 * j + 1];
+    v[2 * j] = q;
+    v[2 * j + 1] = lam[j] - p;
+    for (int k = j + 1; k < 4; ++k) {  // (A_kk - lambda) v_k = -sum_{l<k} A_kl v_l
+      cd r0 = 0, r1 = 0;
+      for (int l = 2 * j; l < 2 * k; ++l) {
+        r0 -= A[(2 * k) * 8 + l] * v[l];
+        r1 -= A[(2 * k + 1) * 8 + l] * v[l];
+      }
+      const cd m00 = A[(2 * k) * 8 + 2 * k] - lam[j], m01 = A[(2 * k) * 8 + 2 * k + 1];
+      const cd m10 = A[(2 * k + 1) * 8 + 2 * k], m11 = A[(2 * k + 1) * 8 + 2 * k + 1] - lam[j];
+      const cd det = m00 * m11 - m01 * m10;
+      v[2 * k] = (r0 * m11 - m01 * r1) / det;
+      v[2 * k + 1] = (m00 * r1 - m10 * r0) / det;
+    }
+    double nrm = 0;
+    int big = 0;
+    for (int i = 0; i < 8; ++i) {
+      nrm += std::norm(v[i]);
+      if (std::abs(v[i]) > std::abs(v[big])) big = i;
+    }
+    const cd rot = std::conj(v[big]) / std::abs(v[big]) / std::sqrt(nrm);
+    for (int i = 0; i < 8; ++i) {
+      const cd w = v[i] * rot;
+      T[i * 8 + 2 * j] = w.real();
+      T[i * 8 + 2 * j + 1] = w.imag();
+    }
   }
-  std::vector<std::vector<double>> Ct(kXtB, std::vector<double>(8));
-  Mat8 At = I;  // A^t
+  Mat8 Ti;
+  mat_inverse8(T, Ti);
+  for (int i = 0; i < 64; ++i) X.ti[i / 8][i % 8] = (float)Ti[i];
+  for (int r = 0; r < 8; ++r) {  // T^-1 (zi), the steady state per unit input
+    double acc = 0;
+    for (int k = 0; k < 8; ++k) acc += Ti[r * 8 + k] * kDecimZi[k / 2][k % 2];
+    X.zim[r] = (float)acc;
+  }
+  Mat8 AtT = T;  // A^t T
   for (int t = 0; t < kXtB; ++t) {
     for (int q = 0; q < 8; ++q) {
       double acc = 0;
-      for (int r = 0; r < 8; ++r) acc += C[r] * At[r * 8 + q];
-      Ct[t][q] = acc;
-      T.Ct[t][q] = (float)acc;
+      for (int r = 0; r < 8; ++r) acc += C[r] * AtT[r * 8 + q];
+      X.cm[t][q] = (float)acc;
     }
-    At = matmul8(At, A);
+    AtT = matmul8(A, AtT);
   }
-  Mat8 ABp = I;  // (A^16)^(63 - lane), built from lane 63 downwards
-  for (int lane = 63; lane >= 0; --lane) {
-    for (int k = 0; k < kXtHeld; ++k)
-      for (int q = 0; q < 8; ++q) {
-        double acc = 0;
-        for (int r = 0; r < 8; ++r) acc += Ct[kXtB - 2 - 2 * k][r] * ABp[r * 8 + q];
-        T.D[lane][k][q] = (float)acc;
-      }
-    ABp = matmul8(ABp, AB);
+  for (int j = 0; j < 4; ++j) {
+    const cd l16 = std::pow(lam[j], kXtB);
+    X.p16[j][0] = (float)l16.real();
+    X.p16[j][1] = (float)l16.imag();
+    for (int d = 0; d < kXtScan; ++d) {
+      const cd w = std::pow(lam[j], kXtB << d);
+      X.scan[d][j][0] = (float)w.real();
+      X.scan[d][j][1] = (float)w.imag();
+    }
+    for (int i = 0; i < 64; ++i) {
+      const cd w = std::pow(lam[j], kXtB * i);
+      X.lag[i][j][0] = (float)w.real();
+      X.lag[i][j][1] = (float)w.imag();
+    }
   }
 }
 
@@ -307,6 +381,8 @@ int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
 constexpr int kEdge = 384;
 int64_t edge_window(int K) { return ((int64_t)1 << K) * (kEdge + 640); }
 
+constexpr int kXtMinFrames = 256;
+
 bool use_fused(const zfft_plan *p, int64_t L) {
   if (p->path == 1 || p->K < 2) return false;
   return 8 * edge_window(p->K) <= L;  // windows cost <= 1/4 of a frame
@@ -413,7 +489,7 @@ int run_xt(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t
     float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
     const InDesc src = k == 0 ? in : InDesc{cur, n[k], n[k], kInC64, 0};
     e = launch_xt_stage(src, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
-                        p->xt_tab.as<XtTables>(), st);
+                        p->xt_tab.as<XtModal>(), st);
     if (e != hipSuccess) return hip_fail(e, "xt_stage launch");
     mark(p, st, k == 0 ? "xt_stage_mix" : "xt_stage");
     cur = dst;
@@ -426,7 +502,10 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
                   const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   int rc = ensure_lo(p, L);
   if (rc) return rc;
-  if (p->path == 3) return run_xt(p, in, frames, n, out, st);
+  // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
+  // blocked schedules split each frame over many waves and win for a few frames per call
+  if (p->path == 3 || (p->path == 0 && frames >= kXtMinFrames))
+    return run_xt(p, in, frames, n, out, st);
   if (use_fused(p, L)) return run_fused(p, in, L, frames, n, out, st);
   return run_exact(p, in, p->lo.as<float2>(), frames, n, out, st);
 }
@@ -592,10 +671,10 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
       e = hipMemcpy(p->tws.p, ts.data(), ts.size() * sizeof(float2), hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) {
-    XtTables xt;
+    XtModal xt;
     xt_build_tables(xt);
-    e = p->xt_tab.ensure(sizeof(XtTables));
-    if (e == hipSuccess) e = hipMemcpy(p->xt_tab.p, &xt, sizeof(XtTables), hipMemcpyHostToDevice);
+    e = p->xt_tab.ensure(sizeof(XtModal));
+    if (e == hipSuccess) e = hipMemcpy(p->xt_tab.p, &xt, sizeof(XtModal), hipMemcpyHostToDevice);
   }
   if (e != hipSuccess) {
     zfft_plan_destroy(p);

@@ -41,6 +41,11 @@ for s in $STEPS; do
       for blk in 512 1024 2048 4096; do
         run sweep_b$blk 300 python bench.py --steps 5 --warmup 1 --no-cpu --block $blk || exit $?
       done ;;
+    bench5)
+      run bench_cfg5_f32 600 python bench.py --config cfg5 --steps 5 --warmup 1 --no-cpu || exit $?
+      run bench_cfg5_f16 600 python bench.py --config cfg5 --steps 5 --warmup 1 --no-cpu --in-dtype complex32 || exit $?
+      run bench_cfg2_f16 600 python bench.py --steps 5 --warmup 1 --no-cpu --in-dtype complex32 || exit $?
+      run bench_cfg2_u8 600 python bench.py --steps 5 --warmup 1 --no-cpu --in-dtype cu8 || exit $? ;;
     bench3)
       run bench_cfg3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu || exit $? ;;
     prof)
