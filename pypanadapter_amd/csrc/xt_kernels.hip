@@ -64,6 +64,33 @@ __device__ __forceinline__ CTab fresh(CTab p) {
   return p;
 }
 
+// Whole-wave DPP shift by one lane (GFX9 wave_shr:1 / wave_shl:1): lane i takes lane i-1
+// (SHR) or i+1 (SHL); the lane without a source keeps `old`.  One VALU op per dword,
+// instead of an LDS-routed ds_bpermute plus a select.
+constexpr int kWaveShr1 = 0x138, kWaveShl1 = 0x130;
+template <int CTRL>
+__device__ __forceinline__ v2f wave_shift(v2f old, v2f src) {
+  return v2f{__int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old.x), __float_as_int(src.x),
+                                                        CTRL, 0xF, 0xF, false)),
+             __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old.y), __float_as_int(src.y),
+                                                        CTRL, 0xF, 0xF, false))};
+}
+
+__device__ __forceinline__ Sos32 load_sos(CTab t) {  // field-wise: scalar loads from AS4
+  Sos32 c;
+  c.b0 = t->sos.b0;
+  c.b1 = t->sos.b1;
+  c.b2 = t->sos.b2;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    c.a1[k] = t->sos.a1[k];
+    c.a2[k] = t->sos.a2[k];
+    c.zi[k][0] = t->sos.zi[k][0];
+    c.zi[k][1] = t->sos.zi[k][1];
+  }
+  return c;
+}
+
 // (a, b) <- [[c, s], [-s, c]] (a, b): one mode times lambda^p = c + i s
 __device__ __forceinline__ void rot(v2f &a, v2f &b, float c, float s) {
   const v2f na = vfma(splat(c), a, splat(s) * b);
@@ -103,14 +130,23 @@ __device__ __forceinline__ void modal_scan(Modal &m, CTab tab, int lane) {
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
     for (int d = 0; d < kLevels[j]; ++d) {
-      const int sh = 1 << d;
-      const bool take = UP ? lane >= sh : lane + sh <= 63;
-      const int src = (UP ? lane - sh : lane + sh) & 63;
-      v2f pa = shfl2(m.r[2 * j], src), pb = shfl2(m.r[2 * j + 1], src);
-      pa = take ? pa : splat(0.f);
-      pb = take ? pb : splat(0.f);
       CTab tb = fresh(tab);
-      rot(pa, pb, tb->scan[d][j][0], tb->scan[d][j][1]);
+      float c = tb->scan[d][j][0], sn = tb->scan[d][j][1];
+      v2f pa, pb;
+      if (d == 0) {  // neighbour lane: DPP shift, zero at the open end
+        constexpr int ctrl = UP ? kWaveShr1 : kWaveShl1;
+        pa = wave_shift<ctrl>(splat(0.f), m.r[2 * j]);
+        pb = wave_shift<ctrl>(splat(0.f), m.r[2 * j + 1]);
+      } else {       // distance 2^d: ds_bpermute, lanes without a source get coefficient 0
+        const int sh = 1 << d;
+        const bool take = UP ? lane >= sh : lane + sh <= 63;
+        const int src = (UP ? lane - sh : lane + sh) & 63;
+        pa = shfl2(m.r[2 * j], src);
+        pb = shfl2(m.r[2 * j + 1], src);
+        c = take ? c : 0.f;
+        sn = take ? sn : 0.f;
+      }
+      rot(pa, pb, c, sn);
       m.r[2 * j] += pa;
       m.r[2 * j + 1] += pb;
     }
@@ -180,10 +216,17 @@ __global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
     const bool fast = base >= kPad && base + kXtT <= n + kPad;  // wave-uniform
     // sample s = lane + 64 q -> row s/16 = lane/16 + 4 q, column lane%16
     v2f *st = lds + (lane >> 4) * kXtLdsStride + (lane & 15);
+    v2f lo0 = splat(0.f);
     if (fast) {
+      // raw samples only: all 16 loads in flight at once (no per-load mixing in between);
+      // the LO is applied after the transpose, per lane on consecutive samples
+      if constexpr (MIX) lo0 = lo[base - kPad + kXtB * lane];
+      v2f raw[kXtB];
 #pragma unroll
-      for (int q = 0; q < kXtB; ++q) st[4 * kXtLdsStride * q] = X(base - kPad + lane + 64 * q);
-    } else {
+      for (int q = 0; q < kXtB; ++q) raw[q] = load_in_t<DT, FLIP>(in, f, base - kPad + lane + 64 * q);
+#pragma unroll
+      for (int q = 0; q < kXtB; ++q) st[4 * kXtLdsStride * q] = raw[q];
+    } else {  // frame edges: odd extension of the mixed signal, built sample by sample
 #pragma unroll
       for (int q = 0; q < kXtB; ++q) st[4 * kXtLdsStride * q] = ext(base + lane + 64 * q);
     }
@@ -193,14 +236,23 @@ __global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
 #pragma unroll
     for (int t = 0; t < kXtB; ++t) y[t] = row[t];
     __builtin_amdgcn_wave_barrier();
+    if constexpr (MIX) {
+      if (fast) {  // lo[i0 + t] = lo[i0] exp(-2 pi i f_lo t / fs), the w^t from the plan
+        const CTab tb = fresh(tab);
+#pragma unroll
+        for (int t = 0; t < kXtB; ++t)
+          y[t] = cmul2(y[t], cmul2(lo0, v2f{tb->wt[t][0], tb->wt[t][1]}));
+      }
+    }
 
     // ---- forward pass ----
     Modal m;
     {
+      const Sos32 cs = load_sos(fresh(tab));
       IirState v;
       state_zero(v);
 #pragma unroll
-      for (int t = 0; t < kXtB; ++t) y[t] = cascade(y[t], v, c);
+      for (int t = 0; t < kXtB; ++t) y[t] = cascade(y[t], v, cs);
       to_modal(tab, v, m);
     }
     {  // lane 0 also carries lambda^16 m_in (the tile's entering state)
@@ -208,17 +260,16 @@ __global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
       Modal u = m_in;
 #pragma unroll
       for (int j = 0; j < 4; ++j) rot(u.r[2 * j], u.r[2 * j + 1], tb->p16[j][0], tb->p16[j][1]);
+      if (lane == 0) {  // exec-masked: 8 packed adds, no selects
 #pragma unroll
-      for (int r = 0; r < 8; ++r) m.r[r] += lane == 0 ? u.r[r] : splat(0.f);
+        for (int r = 0; r < 8; ++r) m.r[r] += u.r[r];
+      }
     }
     modal_scan<true>(m, tab, lane);
     {
       Modal me;  // state entering this lane's sub-block
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const v2f up = shfl2(m.r[r], (lane + 63) & 63);
-        me.r[r] = lane == 0 ? m_in.r[r] : up;
-      }
+      for (int r = 0; r < 8; ++r) me.r[r] = wave_shift<kWaveShr1>(m_in.r[r], m.r[r]);
 #pragma unroll
       for (int r = 0; r < 8; ++r) m_in.r[r] = lane_of(m.r[r], 63);  // next tile's entering state
 #pragma unroll
@@ -242,11 +293,12 @@ __global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
     }
     v2f kept[kXtHeld];
     {
+      const Sos32 cs = load_sos(fresh(tab));
       IirState v;
       state_zero(v);
 #pragma unroll
       for (int t = kXtB - 1; t >= 0; --t) {
-        const v2f yb = cascade(y[t], v, c);
+        const v2f yb = cascade(y[t], v, cs);
         if (t & 1) kept[t >> 1] = yb;  // j = base + 16 lane + t odd <=> (j - 27) even
       }
       to_modal(tab, v, m);
@@ -259,17 +311,16 @@ __global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
       Modal u = qtop;
 #pragma unroll
       for (int j = 0; j < 4; ++j) rot(u.r[2 * j], u.r[2 * j + 1], tb->p16[j][0], tb->p16[j][1]);
+      if (lane == 63) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) m.r[r] += lane == 63 ? u.r[r] : splat(0.f);
+        for (int r = 0; r < 8; ++r) m.r[r] += u.r[r];
+      }
     }
     modal_scan<false>(m, tab, lane);
     {
       Modal qe;  // state entering this lane's sub-block from above
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const v2f dn = shfl2(m.r[r], (lane + 1) & 63);
-        qe.r[r] = lane == 63 ? qtop.r[r] : dn;
-      }
+      for (int r = 0; r < 8; ++r) qe.r[r] = wave_shift<kWaveShl1>(qtop.r[r], m.r[r]);
 #pragma unroll
       for (int k = 0; k < kXtHeld; ++k) kept[k] = dot_cm(fresh(tab), kXtB - 2 - 2 * k, qe, kept[k]);
     }

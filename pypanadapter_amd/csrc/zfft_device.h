@@ -15,6 +15,15 @@ __device__ __forceinline__ v2f cmul(v2f a, v2f b) {
   return v2f{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
 }
 
+// a * b in two VOP3P instructions: t = (a.x b.x, a.x b.y); (a.y (-b.y), a.y b.x) + t
+__device__ __forceinline__ v2f cmul2(v2f a, v2f b) {
+  v2f t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef unsigned char u8x2 __attribute__((ext_vector_type(2)));
 

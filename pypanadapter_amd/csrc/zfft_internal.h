@@ -85,6 +85,8 @@ struct XtModal {
   float p16[4][2];         // lambda_j^16 (re, im): one lane sub-block
   float scan[kXtScan][4][2];  // lambda_j^(16 * 2^d): scan level d
   float lag[64][4][2];     // lambda_j^(16 i): i sub-blocks down from the tile top
+  float wt[kXtB][2];       // exp(-2 pi i f_lo t / fs), t < 16: the LO across one sub-block
+  Sos32 sos;               // the cascade, read per pass (not pinned in SGPRs for the kernel)
 };
 
 hipError_t launch_xt_stage(const InDesc &in, int n, const float2 *lo, bool mix,

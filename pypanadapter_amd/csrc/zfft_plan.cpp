@@ -673,6 +673,12 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
   if (e == hipSuccess) {
     XtModal xt;
     xt_build_tables(xt);
+    xt.sos = sos32();
+    for (int t = 0; t < kXtB; ++t) {  // LO step across a sub-block (lo[n] = sqrt2 w^n)
+      const double ph = -2.0 * M_PI * std::fmod((double)t * c.f_lo / c.fs, 1.0);
+      xt.wt[t][0] = (float)std::cos(ph);
+      xt.wt[t][1] = (float)std::sin(ph);
+    }
     e = p->xt_tab.ensure(sizeof(XtModal));
     if (e == hipSuccess) e = hipMemcpy(p->xt_tab.p, &xt, sizeof(XtModal), hipMemcpyHostToDevice);
   }
