@@ -84,9 +84,11 @@ def _share_hip_runtime_with_torch() -> None:
         ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
 
 
-def load(path: str = LIB_PATH):
-    """Load libzfft.so; raises OSError (loudly) when it has not been built."""
+def load(path: str = ""):
+    """Load libzfft.so; raises OSError (loudly) when it has not been built.  ZFFT_LIB_PATH
+    selects another in-tree build of the same library (A/B of build variants)."""
     global _lib
+    path = path or os.environ.get("ZFFT_LIB_PATH") or LIB_PATH
     if _lib is not None:
         return _lib
     _share_hip_runtime_with_torch()

@@ -23,20 +23,24 @@ def needs_build() -> bool:
     return not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < _newest_input_mtime()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH,
+          defines: tuple = ()) -> str:
+    """hipcc all sources into `out`; `defines` ("NAME=VALUE", ...) select kernel build knobs
+    (A/B variants written elsewhere than the shipped LIB_PATH)."""
+    if not force and not defines and out == LIB_PATH and not needs_build():
         return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
-    tmp = LIB_PATH + ".tmp"
+    tmp = out + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    cmd += [f"-D{d}" for d in defines]
     cmd += [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

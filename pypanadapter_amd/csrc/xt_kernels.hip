@@ -30,6 +30,19 @@
 namespace zfft {
 
 constexpr int kXtLdsStride = kXtB + 1;      // padded sub-block rows: conflict-free ds_read_b64
+
+// Build knobs (A/B of register allocation vs. constant refetch; defaults are the shipped
+// choice): XT_WAVES = waves per SIMD the kernel is compiled for; XT_CM_GROUP = output rows
+// per refetch of the C A^t T table; XT_SCAN_FRESH = refetch the scan coefficients per level.
+#ifndef XT_WAVES
+#define XT_WAVES 4
+#endif
+#ifndef XT_CM_GROUP
+#define XT_CM_GROUP 1
+#endif
+#ifndef XT_SCAN_FRESH
+#define XT_SCAN_FRESH 1
+#endif
 constexpr int kLevels[4] = {2, 2, 3, kXtScan};
 
 struct Modal {
@@ -130,7 +143,7 @@ __device__ __forceinline__ void modal_scan(Modal &m, CTab tab, int lane) {
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
     for (int d = 0; d < kLevels[j]; ++d) {
-      CTab tb = fresh(tab);
+      CTab tb = XT_SCAN_FRESH ? fresh(tab) : tab;
       float c = tb->scan[d][j][0], sn = tb->scan[d][j][1];
       v2f pa, pb;
       if (d == 0) {  // neighbour lane: DPP shift, zero at the open end
@@ -154,7 +167,7 @@ __device__ __forceinline__ void modal_scan(Modal &m, CTab tab, int lane) {
 }
 
 template <bool MIX, int DT, int FLIP>  // DT, FLIP: input format (stage 0 reads the caller's frames)
-__global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
+__global__ __launch_bounds__(256, XT_WAVES) void xt_stage_kernel(InDesc in, int n,
                                                        const v2f *__restrict__ lo,
                                                        v2f *__restrict__ out, int frames,
                                                        const XtModal *tab_g,
@@ -273,7 +286,11 @@ __global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
 #pragma unroll
       for (int r = 0; r < 8; ++r) m_in.r[r] = lane_of(m.r[r], 63);  // next tile's entering state
 #pragma unroll
-      for (int t = 0; t < kXtB; ++t) y[t] = dot_cm(fresh(tab), t, me, y[t]);
+      for (int t0 = 0; t0 < kXtB; t0 += XT_CM_GROUP) {
+        const CTab tb = fresh(tab);
+#pragma unroll
+        for (int t = t0; t < t0 + XT_CM_GROUP; ++t) y[t] = dot_cm(tb, t, me, y[t]);
+      }
     }
 
     // ---- backward pass ----
@@ -322,7 +339,12 @@ __global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
 #pragma unroll
       for (int r = 0; r < 8; ++r) qe.r[r] = wave_shift<kWaveShl1>(qtop.r[r], m.r[r]);
 #pragma unroll
-      for (int k = 0; k < kXtHeld; ++k) kept[k] = dot_cm(fresh(tab), kXtB - 2 - 2 * k, qe, kept[k]);
+      for (int k0 = 0; k0 < kXtHeld; k0 += XT_CM_GROUP) {
+        const CTab tb = fresh(tab);
+#pragma unroll
+        for (int k = k0; k < k0 + XT_CM_GROUP && k < kXtHeld; ++k)
+          kept[k] = dot_cm(tb, kXtB - 2 - 2 * k, qe, kept[k]);
+      }
     }
     // ---- the tile below is now complete: its top state is this tile's bottom state ----
     if (tau > 0) {
@@ -332,7 +354,12 @@ __global__ __launch_bounds__(256, 4) void xt_stage_kernel(InDesc in, int n,
 #pragma unroll
       for (int j = 0; j < 4; ++j) rot(q.r[2 * j], q.r[2 * j + 1], lgc[j], lgs[j]);
 #pragma unroll
-      for (int k = 0; k < kXtHeld; ++k) held[k] = dot_cm(fresh(tab), kXtB - 2 - 2 * k, q, held[k]);
+      for (int k0 = 0; k0 < kXtHeld; k0 += XT_CM_GROUP) {
+        const CTab tb = fresh(tab);
+#pragma unroll
+        for (int k = k0; k < k0 + XT_CM_GROUP && k < kXtHeld; ++k)
+          held[k] = dot_cm(tb, kXtB - 2 - 2 * k, q, held[k]);
+      }
       store_kept(tau - 1, held);
     }
 #pragma unroll

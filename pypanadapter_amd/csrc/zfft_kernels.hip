@@ -555,8 +555,11 @@ __device__ __forceinline__ int stockham_out_index(int t, int N, int Ns, int i) {
 // pass; then radix-16 Stockham passes through LDS; the last pass accumulates |X|^2 in
 // registers for every bin the thread owns.  The next segment's loads are issued before
 // the current FFT (register prefetch).  Finally: density scale, fftshift crop, 20 log10.
+#ifndef WELCH_MINB
+#define WELCH_MINB 1
+#endif
 template <int R0, bool PF, int MAXT>  // PF: register prefetch of the next segment
-__global__ __launch_bounds__(MAXT) void welch_rows_kernel(const v2f *__restrict__ x, int64_t len,
+__global__ __launch_bounds__(MAXT, (MAXT == 256 ? WELCH_MINB : 1)) void welch_rows_kernel(const v2f *__restrict__ x, int64_t len,
                                                           const float *__restrict__ win,
                                                           const v2f *__restrict__ tw,
                                                           WelchGeom g, float *__restrict__ rows,
@@ -914,7 +917,10 @@ template <int R0>
 static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
                                const WelchGeom &g, float *rows, int frames, hipStream_t st) {
   // threads = N/16 (>= 64): N <= 4096 -> <= 256 threads, room for the prefetch registers
-  if (g.n_fft <= 4096) return welch_launch_t<R0, true, 256>(x, len, win, tw, g, rows, frames, st);
+#ifndef WELCH_PF
+#define WELCH_PF 1
+#endif
+  if (g.n_fft <= 4096) return welch_launch_t<R0, WELCH_PF != 0, 256>(x, len, win, tw, g, rows, frames, st);
   if (g.n_fft <= 8192) return welch_launch_t<R0, false, 512>(x, len, win, tw, g, rows, frames, st);
   return welch_launch_t<R0, false, 1024>(x, len, win, tw, g, rows, frames, st);
 }
