@@ -58,7 +58,11 @@ enum zfft_window_kind {
   ZFFT_WIN_KAISER = 12,           /* window_param[0] = beta              */
   ZFFT_WIN_GAUSSIAN = 13,         /* window_param[0] = std               */
   ZFFT_WIN_GENERAL_GAUSSIAN = 14, /* window_param = {p, sig}              */
-  ZFFT_WIN_TUKEY = 15,            /* window_param[0] = alpha             */
+  ZFFT_WIN_TUKEY = 15,            /* window_param[0] = alpha (NaN: 0.5)  */
+  ZFFT_WIN_EXPONENTIAL = 16,      /* window_param = {center, tau}; NaN = scipy default
+                                     (get_window(('exponential', 3), N) binds 3 to center) */
+  ZFFT_WIN_CHEBWIN = 17,          /* window_param[0] = attenuation, dB   */
+  ZFFT_WIN_DPSS = 18,             /* window_param[0] = NW (single taper)  */
   ZFFT_WIN_ARRAY = 100            /* caller-supplied float window (any scipy window) */
 };
 
@@ -69,7 +73,7 @@ typedef struct zfft_config {
   int32_t window_kind;     /* enum zfft_window_kind                                         */
   double fs;               /* sample rate, Hz (panadapter.SampleRate)                       */
   double f_lo;             /* LO frequency, Hz; the reference hard-codes 1.0 (S:2090)       */
-  double window_param[2];  /* see window kinds                                              */
+  double window_param[2];  /* see window kinds; NaN = parameter absent (scipy's default)      */
   int32_t scroll;          /* waterfall direction, +1 or -1 (AppState.scroll, S:1496)       */
   int32_t in_dtype;        /* 0 = complex64 (interleaved f32, 8 B/sample); 1 = complex32
                               (interleaved f16, 4 B/sample, BASELINE cfg5); 2 = RTL-SDR

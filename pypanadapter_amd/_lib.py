@@ -23,7 +23,8 @@ ZFFT_EUNSUPPORTED = -6
 WINDOW_KINDS = {
     "hamming": 0, "hann": 1, "blackman": 2, "blackmanharris": 3, "nuttall": 4, "flattop": 5,
     "barthann": 6, "bartlett": 7, "triang": 8, "bohman": 9, "parzen": 10, "boxcar": 11,
-    "kaiser": 12, "gaussian": 13, "general_gaussian": 14, "tukey": 15,
+    "kaiser": 12, "gaussian": 13, "general_gaussian": 14, "tukey": 15, "exponential": 16,
+    "chebwin": 17, "dpss": 18,
 }
 # scipy.signal.get_window aliases (scipy/signal/windows/_windows.py `_win_equiv`)
 WINDOW_ALIASES = {
@@ -35,7 +36,7 @@ WINDOW_ALIASES = {
     "par": "parzen", "box": "boxcar", "ones": "boxcar", "rect": "boxcar", "rectangular": "boxcar",
     "ksr": "kaiser", "gauss": "gaussian", "gss": "gaussian", "general gaussian": "general_gaussian",
     "general gauss": "general_gaussian", "general_gauss": "general_gaussian", "ggs": "general_gaussian",
-    "tuk": "tukey",
+    "tuk": "tukey", "poisson": "exponential", "cheb": "chebwin",
 }
 WIN_ARRAY = 100
 

@@ -19,7 +19,9 @@ def _window_spec(window):
     """AppState.fft_tapering value -> (kind, params, array_or_None).
 
     Accepts what the reference stores (S:1358-1363): a scipy window name, a
-    (name, p0[, p1]) tuple, or an explicit array (any scipy window, e.g. chebwin/dpss).
+    (name, p0[, p1]) tuple, or an explicit array (any other scipy window).  Absent
+    parameters are NaN: the native generator applies scipy's default or refuses the window
+    as get_window does.
     """
     if isinstance(window, np.ndarray) or (isinstance(window, (list,)) and window and
                                           not isinstance(window[0], str)):
@@ -29,7 +31,9 @@ def _window_spec(window):
     if name not in _lib.WINDOW_KINDS:
         raise ValueError(f"window {window!r} has no native generator; pass it as an array "
                          "(e.g. scipy.signal.get_window(window, n_fft))")
-    p = [float(v) for v in params] + [0.0, 0.0]
+    if len(params) > 2:
+        raise ValueError(f"window {window!r}: at most two parameters")
+    p = [float(v) for v in params] + [float("nan")] * 2
     return _lib.WINDOW_KINDS[name], (p[0], p[1]), None
 
 

@@ -23,10 +23,7 @@ def _gpu(zfft_lib):
 
 def _plan_for(c, **kw):
     from pypanadapter_amd import ZoomFFT
-    w = window_of(c["window"])
-    if (isinstance(w, tuple) and w[0] in ("chebwin", "dpss")) or w in ("chebwin", "dpss"):
-        import scipy.signal as ss
-        w = ss.get_window(w, c["n_fft"])  # no native generator: caller array (ZFFT_WIN_ARRAY)
+    w = window_of(c["window"])  # every taper-list window is generated natively
     return ZoomFFT(c["n_fft"], c["zoom"], c["fs"], n_win=c["n_win"], window=w, f_lo=c["f_lo"], **kw)
 
 
@@ -67,6 +64,19 @@ def test_golden_rows_four_step_welch():
                 with pytest.raises(NotImplementedError):
                     plan.set_welch(1)
         assert_row_close(row, golden_rows()[c["name"]], f"{c['name']} four-step")
+
+
+def test_array_windows_reproduce_golden_rows():
+    """ZFFT_WIN_ARRAY (any scipy window handed over as values) gives the same rows."""
+    import scipy.signal as ss
+    from pypanadapter_amd import ZoomFFT
+    for c in CASES:
+        if not c["name"].startswith("win_"):
+            continue
+        w = ss.get_window(window_of(c["window"]), c["n_fft"])
+        with ZoomFFT(c["n_fft"], c["zoom"], c["fs"], n_win=c["n_win"], window=w) as plan:
+            row = plan.rows(case_input(c))
+        assert_row_close(row, golden_rows()[c["name"]], f"{c['name']} as array")
 
 
 def test_zoomfft_fixtures():

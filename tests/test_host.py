@@ -70,7 +70,13 @@ def test_nodev_is_loud(zfft_lib):
 WINDOWS = ["hamming", "hann", "blackman", "blackmanharris", "nuttall", "flattop", "barthann",
            "bartlett", "triang", "bohman", "parzen", "boxcar", ("kaiser", 14), ("gaussian", 7),
            ("general_gaussian", 1.5, 7), ("tukey", 0.3), ("tukey", 0.0), ("tukey", 1.0),
-           ("kaiser", 0.5), "han", "rect", "bmn", ("general gaussian", 2, 5)]
+           ("kaiser", 0.5), "han", "rect", "bmn", ("general gaussian", 2, 5), "tukey",
+           ("exponential", 3), "exponential", ("exponential", 3, 2.5), "poisson"]
+# windows computed through a solver / DFT, compared with scipy's LAPACK / pocketfft results
+# to 5e-9 of the window maximum (fp32 rounding is 6e-8): the taper list's dpss and chebwin.
+# dpss is conditioning-limited: at M=32768, NW=0.7 the top two eigenvalues of the
+# tridiagonal differ by 6e-9 relative, so any fp64 eigenvector is only good to ~1e-9.
+SOLVED = [("dpss", 3), ("dpss", 1.5), ("dpss", 0.7), ("chebwin", 100), ("cheb", 50)]
 
 
 @pytest.mark.parametrize("win", WINDOWS, ids=str)
@@ -83,10 +89,40 @@ def test_native_windows_match_scipy(zfft_lib, win, M):
     np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-14)
 
 
-def test_unknown_window_needs_array():
+@pytest.mark.parametrize("win", SOLVED, ids=str)
+@pytest.mark.parametrize("M", [7, 64, 584, 1000, 4096, 32768])
+def test_native_solved_windows_match_scipy(zfft_lib, win, M):
+    import scipy.signal as ss
+    from pypanadapter_amd import native_window
+    ref = ss.get_window(win, M)
+    got = native_window(win, M)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=5e-9)
+
+
+@pytest.mark.parametrize("M", [65536, 4097])
+def test_native_chebwin_long(zfft_lib, M):
+    """chebwin's DFT runs at any length (Bluestein); cfg5 uses nperseg = 65536, whose
+    extended length 65537 is prime (pocketfft takes Bluestein there too).  Agreement to
+    2e-8 of the maximum: under the fp32 rounding (6e-8) the kernels see."""
+    import scipy.signal as ss
+    from pypanadapter_amd import native_window
+    np.testing.assert_allclose(native_window(("chebwin", 100), M),
+                               ss.get_window(("chebwin", 100), M), rtol=0, atol=2e-8)
+
+
+def test_window_refusals_follow_scipy(zfft_lib):
+    """Windows get_window refuses are refused (ValueError), not silently defaulted."""
+    import scipy.signal as ss
+    from pypanadapter_amd import native_window
     from pypanadapter_amd.engine import _window_spec
-    with pytest.raises(ValueError):
-        _window_spec(("chebwin", 100))
+    for win, M in [("kaiser", 64), ("gaussian", 64), ("chebwin", 64), ("dpss", 64),
+                   (("dpss", 40), 64), (("general_gaussian", 1.5), 64)]:
+        with pytest.raises((ValueError, TypeError)):  # general_gaussian without sig: TypeError
+            ss.get_window(win, M)
+        with pytest.raises(ValueError):
+            native_window(win, M)
+    with pytest.raises(ValueError):  # slepian: unknown to scipy 1.15 as well (SURVEY §8a-8)
+        _window_spec(("slepian", 0.3))
     kind, _, arr = _window_spec(np.hanning(16))
     assert kind == 100 and arr.dtype == np.float32
 
