@@ -1,0 +1,720 @@
+// xa_kernels.hip -- "XA" zero-phase decimation stage for gfx950 (design model:
+// tools/xa_proto.py; tables: zfft_plan.cpp xa_build_tables).
+//
+// One stage of the reference's decimate(x, 2) (pypanadapter_spectrum.py:2096-2098 ->
+// scipy sosfiltfilt: odd pad 27, steady-state initial conditions, forward + backward,
+// [::2]) on one frame per wave, reading the stage input once and writing only the
+// decimated output.  The cascade H = N(z)/D(z) is factored (exactly, edges included) as
+//
+//   v = ext / D(z)                         forward all-pole cascade, input rate
+//   h_j = sum_t M_t v[j-8+t], j odd        25-tap FIR M = N(z) N(1/z) D(-1/z), kept j only
+//   g = h / D2(1/w)                        backward all-pole cascade, output rate
+//
+// so a stage costs 8 + 12.5 + 4 packed multiply-adds per input sample, against 2 x 17 for
+// two DF2T passes.  A wave walks its frame in tiles of 64 lanes x 32 samples:
+//  forward:   every lane runs the all-pole cascade from a zero state over its 32 samples;
+//             its end state goes to the real modal basis (T^-1, block lower triangular,
+//             one rotation-scaling 2x2 block per pole pair), a Kogge-Stone scan over
+//             lanes -- per mode only as deep as its radius needs (.935 .808 .682 .587 ->
+//             4 2 1 1 levels) -- gives each lane its entering state, and the outputs get
+//             C A^t T m_in.  The tile's entering state is folded into lane 0.
+//  FIR:       the corrected v go to LDS; lane i evaluates h at the 16 odd positions of
+//             [32i - 16, 32i + 16) from v[32i - 24, 32i + 32): its own row and the last
+//             24 samples of row i-1 (row -1 = the previous tile's row 63, kept in LDS).
+//  backward:  the same scheme on the 16 h values of each lane, descending, with the
+//             state entering the tile from above provisionally zero; the state it leaves
+//             at the tile bottom is exact regardless (its dependence on the top state is
+//             |lambda^2|^512 < 1e-29) and is the top state of the tile below, processed
+//             one step earlier: that tile's top kXaLag outputs get C A2^d T q, then all
+//             its outputs are stored.
+//  frame end: the forward pre-history is the steady state of constant ext[0]
+//             (sosfilt_zi * ext[0]); the backward post-history is the steady state of
+//             constant f[e-1], f = N v formed explicitly for the last 16 positions, whose
+//             h use the unmerged form N(1/z) D(-1/z) on f clamped at e-1.
+// Numerics: float32, max relative error ~8e-6 of the decimated IQ vs float64 sosfiltfilt
+// (plain float32 sosfiltfilt: ~1e-6); end-to-end rows within 1e-5 dB (tools/xa_proto.py).
+#include <cstddef>
+
+#include "zfft_device.h"
+
+#ifndef XA_STAMPS
+#define XA_STAMPS 0
+#endif
+
+namespace zfft {
+namespace xa {
+
+constexpr int kRow = kXaB + 2;          // LDS row stride (v2f): ds_read_b128 rows conflict-free
+constexpr int kHalfRows = 32;           // transposes go through LDS one half tile at a time
+constexpr int kBuf = kHalfRows * kRow + 16 + 64 + 32;  // + FIR carry (12 used) + frame-end v carry + LO chunk starts
+constexpr int kHeldRow = kXaK + 2;      // output-transpose rows (v2f): b128 writes conflict-free
+constexpr int kWaves = 2;               // waves (frames) per workgroup
+#ifndef XA_WAVES
+#define XA_WAVES 2                      // waves per SIMD the register budget is cut for
+#endif
+#ifndef XA_PF
+#define XA_PF 32                        // input chunks of the next tile loaded a tile ahead
+#endif
+#ifndef XA_SPREAD
+#define XA_SPREAD 1                     // next-tile loads in 8 groups spread over the tile
+#endif
+#ifndef XA_LAG_EARLY
+#define XA_LAG_EARLY 1                  // lag rows loaded before the backward pass
+#endif
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+// The filter tables live in LDS (one copy per workgroup, uniform-address broadcast reads
+// into VGPRs, pipelined by the compiler): as scalar K$ reads they cost ~150 s_load +
+// lgkmcnt waits per tile, the largest stall of the loop.  The far-field `lag` rows stay
+// in global memory (per-lane rows).
+typedef const XaTab __attribute__((address_space(3))) *CT;
+constexpr int kTabWords = (int)(offsetof(XaTab, lag) / sizeof(float) + 3) / 4 * 4;
+// an opaque copy per phase: reads are not hoisted out of the tile loop (which would pin
+// ~100 table values in VGPRs), each phase re-reads the few it needs
+typedef const XaTab __attribute__((address_space(4))) *CS;  // scalar reads (global copy)
+__device__ __forceinline__ CS fresh_s(CS p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ CT fresh(CT p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+
+// Raw input element of each in_dtype: tile loads are issued one tile ahead and converted
+// only when consumed, so no conversion (and no wait) sits behind the load.
+template <int DT> struct Raw;
+template <> struct Raw<kInC64> { typedef v2f T; };
+template <> struct Raw<kInC32H> { typedef h2 T; };
+template <> struct Raw<kInCU8> { typedef u8x2 T; };
+template <int DT>
+__device__ __forceinline__ v2f cvt_raw(typename Raw<DT>::T r) {  // as load_in_t (zfft_device.h)
+  if constexpr (DT == kInC64) return r;
+  else if constexpr (DT == kInC32H) return v2f{(float)r.x, (float)r.y};
+  else return v2f{((float)r.x - 127.5f) * (1.f / 127.5f), ((float)r.y - 127.5f) * (1.f / 127.5f)};
+}
+
+struct Md {
+  v2f r[8];  // a0 b0 a1 b1 a2 b2 a3 b3 per mode (I and Q share the real basis)
+};
+
+__device__ __forceinline__ float uni(float a) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(a)));
+}
+__device__ __forceinline__ v2f lane_of(v2f v, int src) {
+  return v2f{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), src)),
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), src))};
+}
+__device__ __forceinline__ v2f shfl2(v2f v, int src) {
+  return v2f{__shfl(v.x, src, 64), __shfl(v.y, src, 64)};
+}
+// whole-wave DPP shift by one lane (wave_shr:1 / wave_shl:1); the lane without a source
+// keeps `old`
+constexpr int kShr1 = 0x138, kShl1 = 0x130;
+template <int CTRL>
+__device__ __forceinline__ v2f wave_shift(v2f old, v2f src) {
+  return v2f{__int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old.x), __float_as_int(src.x),
+                                                        CTRL, 0xF, 0xF, false)),
+             __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old.y), __float_as_int(src.y),
+                                                        CTRL, 0xF, 0xF, false))};
+}
+
+// (a, b) <- [[c, s], [-s, c]] (a, b): one mode times lambda^p = c + i s
+__device__ __forceinline__ void rot(v2f &a, v2f &b, float c, float s) {
+  const v2f na = vfma(splat(c), a, splat(s) * b);
+  b = vfma(splat(c), b, splat(-s) * a);
+  a = na;
+}
+
+// One sample through the all-pole cascade; s[2k] = y_k[t-1], s[2k+1] = y_k[t-2].
+__device__ __forceinline__ v2f ap_step(v2f x, v2f s[8], const float a1[4], const float a2[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // the y[t-2] term first: one multiply-add of latency per step on the recurrence
+    const v2f y = vfma(splat(-a1[k]), s[2 * k], vfma(splat(-a2[k]), s[2 * k + 1], x));
+    s[2 * k + 1] = s[2 * k];
+    s[2 * k] = y;
+    x = y;
+  }
+  return x;
+}
+
+template <int PASS>  // 0 forward, 1 backward
+__device__ __forceinline__ const XaPass __attribute__((address_space(3))) &pass_of(CT t) {
+  if constexpr (PASS == 0) return t->f;
+  else return t->b;
+}
+
+template <int PASS>
+__device__ __forceinline__ void load_ap(CT tab, float a1[4], float a2[4]) {
+  CT t = fresh(tab);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    a1[k] = pass_of<PASS>(t).a1[k];
+    a2[k] = pass_of<PASS>(t).a2[k];
+  }
+}
+
+// m = T^-1 s; T^-1 is block lower triangular (mode j depends on sections <= j)
+template <int PASS>
+__device__ __forceinline__ void to_modal(CT tab, const v2f s[8], Md &m) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    CT t = fresh(tab);
+    v2f acc = splat(0.f);
+#pragma unroll
+    for (int q = 0; q < (r | 1) + 1; ++q) acc = vfma(splat(pass_of<PASS>(t).ti[r][q]), s[q], acc);
+    m.r[r] = acc;
+  }
+}
+
+// inclusive weighted scan over lanes: UP (lane i sums lanes j <= i) or down (j >= i),
+// m_i = sum_j lambda^(S |i-j|) m_j per mode
+template <int PASS, bool UP>
+__device__ __forceinline__ void modal_scan(Md &m, CT tab, int lane) {
+  asm volatile("" : "+v"(lane));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int d = 0; d < kXaLevels[j]; ++d) {
+      CT t = fresh(tab);
+      float c = pass_of<PASS>(t).scan[d][j][0], sn = pass_of<PASS>(t).scan[d][j][1];
+      v2f pa, pb;
+      if (d == 0) {
+        constexpr int ctrl = UP ? kShr1 : kShl1;
+        pa = wave_shift<ctrl>(splat(0.f), m.r[2 * j]);
+        pb = wave_shift<ctrl>(splat(0.f), m.r[2 * j + 1]);
+      } else {
+        const int sh = 1 << d;
+        const bool take = UP ? lane >= sh : lane + sh <= 63;
+        const int src = (UP ? lane - sh : lane + sh) & 63;
+        pa = shfl2(m.r[2 * j], src);
+        pb = shfl2(m.r[2 * j + 1], src);
+        c = take ? c : 0.f;
+        sn = take ? sn : 0.f;
+      }
+      rot(pa, pb, c, sn);
+      m.r[2 * j] += pa;
+      m.r[2 * j + 1] += pb;
+    }
+  }
+}
+
+// the state entering a lane, rotated over one sub-block and folded into that lane's end
+// state before the scan
+template <int PASS>
+__device__ __forceinline__ void fold_entering(Md &m, const Md &in, CT tab, bool here) {
+  CT t = fresh(tab);
+  Md u = in;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rot(u.r[2 * j], u.r[2 * j + 1], pass_of<PASS>(t).pS[j][0], pass_of<PASS>(t).pS[j][1]);
+  if (here) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) m.r[r] += u.r[r];
+  }
+}
+
+// Diagnostic build only (-DXA_STAMPS=1, tools/build_variants.py): per-phase s_memtime
+// sums of every wave, read back with zfft_debug_xa_stamps; no stamp exists otherwise.
+constexpr int kStampSegs = 10;
+#if XA_STAMPS
+__device__ unsigned long long g_xa_stamps[kStampSegs + 1];
+#define XA_STAMP(i)                                                                   \
+  {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    unsigned long long t_;                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    st_acc[i] += t_ - t_prev;                                                         \
+    t_prev = t_;                                                                      \
+  }
+#else
+#define XA_STAMP(i)
+#endif
+
+// modal -> DF-I state, s = T m (T block lower triangular: section k from modes <= k)
+template <int PASS>
+__device__ __forceinline__ void from_modal(CT tab, const Md &m, v2f s[8]) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    CT t = fresh(tab);
+    v2f acc = splat(0.f);
+#pragma unroll
+    for (int q = 0; q < (r | 1) + 1; ++q) acc = vfma(splat(pass_of<PASS>(t).t[r][q]), m.r[q], acc);
+    s[r] = acc;
+  }
+}
+
+template <bool MIX, int DT, int FLIP>
+__global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc in, int n,
+                                                                        const v2f *__restrict__ lo,
+                                                                        v2f *__restrict__ out, int frames,
+                                                                        const XaTab *tab_g) {
+  __shared__ __attribute__((aligned(16))) v2f lds_all[kWaves][kBuf];
+  __shared__ __attribute__((aligned(16))) float ltab[kTabWords];
+  for (int i = threadIdx.x; i < kTabWords / 4; i += 64 * kWaves)
+    ((v4f *)ltab)[i] = ((const v4f *)tab_g)[i];
+  __syncthreads();
+  const CT tab = (CT)(const XaTab __attribute__((address_space(3))) *)ltab;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR
+  const int f = blockIdx.x * kWaves + wv;
+  if (f >= frames) return;  // whole wave
+  v2f *const buf0 = lds_all[wv];            // half-tile transposes: 32 rows of kRow v2f
+  v2f *buf = buf0;
+  v2f *pcarry = buf + kHalfRows * kRow;     // lane 63's FIR neighbour part, for next lane 0
+  v2f *vcarry = pcarry + 16;                // rows 62, 63 of the tile before the last
+  v2f *cq = vcarry + 64;                    // lo at the 32 chunk starts of the tile
+  const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
+  const int nt = (e + 15) / kXaT + 1;  // the last FIR/backward tile reaches e - 1
+  v2f *__restrict__ o = out + (int64_t)f * n_out;
+  auto X = [&](int i) -> v2f {
+    v2f v = load_in_t<DT, FLIP>(in, f, i);
+    if constexpr (MIX) v = cmul(v, lo[i]);
+    return v;
+  };
+  auto ext = [&](int j) -> v2f {  // scipy odd_ext by 27 (_arraytools.py:57); 0 beyond e
+    if (j < kPad) return 2.f * X(0) - X(kPad - j);
+    if (j < n + kPad) return X(j - kPad);
+    if (j < e) return 2.f * X(n - 1) - X(2 * n + kPad - 2 - j);
+    return splat(0.f);
+  };
+
+  const v2f x0 = v2f{uni(ext(0).x), uni(ext(0).y)};
+  Md m_in;  // modal state entering the current tile (forward), wave-uniform
+#pragma unroll
+  for (int r = 0; r < 8; ++r) m_in.r[r] = tab->f.ss[r] * x0;
+  {  // v pre-history (steady output for constant ext[0]): the FIR part lane -1 owes lane 0
+    const v2f vs = tab->vss * x0;
+    if (lane < kXaK) {
+      CT tb = fresh(tab);
+      v2f acc = splat(0.f);
+      for (int t = 0; t < 25; ++t)  // taps on W[m], 1 <= m <= 23, of output k = lane
+        if (2 * lane + t + 1 < 24) acc = vfma(splat(tb->m25[t]), vs, acc);
+      pcarry[lane] = acc;
+    }
+    vcarry[lane] = vs;
+  }
+  __builtin_amdgcn_wave_barrier();
+
+  // Tile outputs -> frame row through LDS transposes (64 consecutive outputs per store
+  // instruction), one half tile at a time.  Chunks below the top kXaLag outputs are final
+  // at once; the top chunks wait in registers for the next tile's exact top state q.
+  constexpr int kChunks = kXaT / 2 / 64;
+  constexpr int kLagChunks = kXaLag / 64;
+  v2f held[kLagChunks];
+#pragma unroll
+  for (int c = 0; c < kLagChunks; ++c) held[c] = splat(0.f);
+  auto m_of = [&](int tile, int idx) { return tile * (kXaT / 2) - (kPad + 15) / 2 + idx; };
+  auto flush_tile = [&](int tile, const v2f *h, int ln) {
+    const int m0 = m_of(tile, ln);
+    v2f *__restrict__ od = o + m0;
+    const bool inside = m_of(tile, 0) >= 0 && m_of(tile, kXaT / 2) <= n_out;  // wave-uniform
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      if ((ln >> 5) == hf) {  // lanes of this half: 16 outputs each into row ln % 32
+        v4f *hw = (v4f *)(buf + (ln & 31) * kHeldRow);
+#pragma unroll
+        for (int k = 0; k < kXaK / 2; ++k) hw[k] = v4f{h[2 * k].x, h[2 * k].y, h[2 * k + 1].x, h[2 * k + 1].y};
+      }
+      __builtin_amdgcn_wave_barrier();
+      // output idx = 64 c + ln (c in this half) sits at row idx/16 - 32 hf, column ln % 16
+      const v2f *hr = buf + (ln >> 4) * kHeldRow + (ln & 15);
+#pragma unroll
+      for (int cc = 0; cc < kChunks / 2; ++cc) {
+        const int c = hf * (kChunks / 2) + cc;
+        const v2f v = hr[cc * 4 * kHeldRow];
+        if (c >= kChunks - kLagChunks) {
+          held[c - (kChunks - kLagChunks)] = v;
+        } else if (inside || (m0 + 64 * c >= 0 && m0 + 64 * c < n_out)) {
+          od[64 * c] = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  };
+  auto finish_held = [&](int tile, const Md *q, const v4f *lg, int ln) {  // + C A2^d T q
+    const int m0 = m_of(tile, (kChunks - kLagChunks) * 64 + ln);
+#pragma unroll
+    for (int c = 0; c < kLagChunks; ++c) {
+      v2f v = held[c];
+      if (q != nullptr) {
+        const v4f l0 = lg[2 * c], l1 = lg[2 * c + 1];
+        v = vfma(splat(l0.x), q->r[0], v);
+        v = vfma(splat(l0.y), q->r[1], v);
+        v = vfma(splat(l0.z), q->r[2], v);
+        v = vfma(splat(l0.w), q->r[3], v);
+        v = vfma(splat(l1.x), q->r[4], v);
+        v = vfma(splat(l1.y), q->r[5], v);
+        v = vfma(splat(l1.z), q->r[6], v);
+        v = vfma(splat(l1.w), q->r[7], v);
+      }
+      const int m = m0 + 64 * c;
+      if (m >= 0 && m < n_out) o[m] = v;
+    }
+  };
+
+  // coalesced tile loads: sample s = 64 q + lane of the tile -> row s/32, in two halves; a
+  // fast tile (inside [27, n + 27): no odd extension) is loaded during the previous tile
+  typedef typename Raw<DT>::T RawT;
+  const RawT *__restrict__ src = (const RawT *)in.p + (int64_t)f * in.stride;
+  auto fast_tile = [&](int b) { return b >= kPad && b + kXaT <= n + kPad; };
+  v2f wl = splat(0.f);  // lo[n0 + l] = lo[n0] w^l: w^l = lo[l] / sqrt(2), per lane
+  if constexpr (MIX) wl = lo[lane] * 0.70710678118654752f;
+  v2f cqv = splat(0.f);  // lo[next tile start - 27 + 64 (lane % 32)], loaded a tile ahead
+  RawT pf[kXaB];  // [0, XA_PF): loaded a tile ahead; the rest at the tile start
+  // next-tile loads: group g = chunks [4g, 4g + 4), issued at 8 points of the tile
+  const RawT *pnext = src;
+  bool next_fast = false;
+  int next_i0 = 0;  // first input index of the next tile
+  auto issue_group = [&](int g) {
+    if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + 64 * (lane & 31)];
+    if (XA_SPREAD && next_fast && 4 * g < XA_PF) {
+#pragma unroll
+      for (int q = 4 * g; q < 4 * g + 4 && q < XA_PF; ++q) pf[q] = pnext[FLIP ? -64 * q : 64 * q];
+    }
+  };
+
+#if XA_STAMPS
+  unsigned long long st_acc[kStampSegs] = {}, t_prev;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_prev)::"memory");
+#endif
+  for (int tau = 0; tau < nt; ++tau) {
+    // an opaque copy of the ln id per tile: ln-derived addresses are recomputed
+    // (a few VALU ops) instead of dozens of them being hoisted and held (or spilled)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    {  // opaque per-tile copy of the LDS base, for the same reason
+      v2f *b = buf0;
+      asm volatile("" : "+s"(b));
+      buf = b;
+      pcarry = buf + kHalfRows * kRow;
+      vcarry = pcarry + 16;
+      cq = vcarry + 64;
+    }
+    const int base = tau * kXaT;
+    const bool last = tau == nt - 1;
+    v2f y[kXaB];
+    {
+      const bool fast = fast_tile(base);  // wave-uniform
+      if (fast && XA_PF < kXaB) {
+        const int i0 = base - kPad + ln;
+        const RawT *p = src + (FLIP ? in.len - 1 - i0 : i0);
+#pragma unroll
+        for (int q = XA_PF; q < kXaB; ++q) pf[q] = p[FLIP ? -64 * q : 64 * q];
+      }
+      if (MIX && fast) {
+        if (ln < 32) cq[ln] = cqv;
+        __builtin_amdgcn_wave_barrier();
+      }
+      v2f *st = buf + (ln >> 5) * kRow + (ln & 31);
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        if (fast) {
+#pragma unroll
+          for (int qq = 0; qq < kXaB / 2; ++qq) {
+            const int q = hf * (kXaB / 2) + qq;
+            v2f x = cvt_raw<DT>(pf[q]);
+            if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl));
+            st[2 * kRow * qq] = x;
+          }
+        } else {
+#pragma unroll 4
+          for (int qq = 0; qq < kXaB / 2; ++qq) st[2 * kRow * qq] = ext(base + ln + 64 * (hf * (kXaB / 2) + qq));
+        }
+        __builtin_amdgcn_wave_barrier();
+        if ((ln >> 5) == hf) {
+          const v4f *rp = (const v4f *)(buf + (ln & 31) * kRow);
+#pragma unroll
+          for (int t = 0; t < kXaB / 2; ++t) {
+            const v4f w = rp[t];
+            y[2 * t] = v2f{w.x, w.y};
+            y[2 * t + 1] = v2f{w.z, w.w};
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    next_fast = tau + 1 < nt && fast_tile(base + kXaT);  // wave-uniform
+    next_i0 = base + kXaT - kPad;
+    {
+      const int i0 = base + kXaT - kPad + ln;
+      pnext = src + (FLIP ? in.len - 1 - i0 : i0);
+    }
+    issue_group(0);
+    XA_STAMP(0);
+
+    // ---- forward all-pole cascade: pass 1 (zero state, end state only), modal scan over
+    //      lanes, pass 2 from the exact entering state, streaming the FIR ----
+    v2f h[kXaK];
+    {
+      Md me;  // state entering this ln's sub-block
+      {
+        Md m;
+        {
+          float a1[4], a2[4];
+          load_ap<0>(tab, a1, a2);
+          v2f s[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) s[r] = splat(0.f);
+#pragma unroll
+          for (int t = 0; t < kXaB; ++t) (void)ap_step(y[t], s, a1, a2);
+          to_modal<0>(tab, s, m);
+        }
+        XA_STAMP(1);
+        issue_group(1);
+        fold_entering<0>(m, m_in, tab, ln == 0);
+        modal_scan<0, true>(m, tab, ln);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) me.r[r] = wave_shift<kShr1>(m_in.r[r], m.r[r]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) m_in.r[r] = lane_of(m.r[r], 63);  // next tile's entering state
+      }
+      XA_STAMP(2);
+      issue_group(2);
+      // FIR at the 16 odd positions p_k = base + 32 ln - 15 + 2k:
+      //   h_k = sum_t M_t W[2k + t + 1],  W[m] = v(32 ln - 24 + m);
+      // W[24 + t] = this ln's v[t]; W[m < 24] = ln-1's v[8 + m], whose share of h_k
+      // ln-1 accumulates itself (P) and hands over with one DPP shift
+      v2f P[12];
+#pragma unroll
+      for (int k = 0; k < kXaK; ++k) h[k] = splat(0.f);
+#pragma unroll
+      for (int k = 0; k < 12; ++k) P[k] = splat(0.f);
+      {
+        float a1[4], a2[4];
+        v2f s[8];
+        from_modal<0>(tab, me, s);
+        // the pass-2 + FIR constants as SGPRs (4 wide scalar loads): this phase holds the
+        // most VGPRs of the tile
+        const CS tbs = fresh_s((CS)tab_g);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          a1[k] = tbs->f.a1[k];
+          a2[k] = tbs->f.a2[k];
+        }
+        float m25s[25];
+#pragma unroll
+        for (int t = 0; t < 25; ++t) m25s[t] = tbs->m25[t];
+#pragma unroll
+        for (int t = 0; t < kXaB; ++t) {
+          if (t == 11) issue_group(3);
+          if (t == 22) issue_group(4);
+          const v2f v = ap_step(y[t], s, a1, a2);
+          y[t] = v;
+#pragma unroll
+          for (int k = 0; k < kXaK; ++k) {
+            const int tap = 24 + t - 1 - 2 * k;
+            if (tap >= 0 && tap < 25) h[k] = vfma(splat(m25s[tap]), v, h[k]);
+          }
+          if (t >= 9) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+              const int tap = t - 8 - 1 - 2 * k;
+              if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), v, P[k]);
+            }
+          }
+        }
+      }
+      {  // neighbour shares: ln i takes ln i-1's P, ln 0 the previous tile's ln 63's
+        const v4f *pc = (const v4f *)pcarry;
+#pragma unroll
+        for (int k2 = 0; k2 < 6; ++k2) {
+          const v4f c4 = pc[k2];
+          h[2 * k2] += wave_shift<kShr1>(v2f{c4.x, c4.y}, P[2 * k2]);
+          h[2 * k2 + 1] += wave_shift<kShr1>(v2f{c4.z, c4.w}, P[2 * k2 + 1]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (ln == 63) {
+          v4f *pw = (v4f *)pcarry;
+#pragma unroll
+          for (int k2 = 0; k2 < 6; ++k2) pw[k2] = v4f{P[2 * k2].x, P[2 * k2].y, P[2 * k2 + 1].x, P[2 * k2 + 1].y};
+        }
+      }
+    }
+    XA_STAMP(3);
+    // frame end: v of the tile before the last (rows 62, 63) and of the last tile's two
+    // lanes around e-25 .. e-1 go to LDS for f = N v.  (`ln`: an opaque ln id, so the
+    // addresses of these once-per-frame paths are not hoisted out of the loop.)
+    const int la = max(0, (e - 25 - base) >> 5);
+    if (tau >= nt - 2) {
+      v2f *dst = nullptr;
+      if (!last && ln >= 62) dst = vcarry + (ln - 62) * 32;
+      if (last && (ln == la || ln == la + 1)) dst = buf + (ln - la) * kRow;
+      if (dst != nullptr) {
+        v4f *wp = (v4f *)dst;
+#pragma unroll
+        for (int t = 0; t < kXaB / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // lag rows for the held tile's top outputs, then the next tile's loads: both land
+    // while the backward pass runs
+    v4f lg[2 * kLagChunks];
+    if (XA_LAG_EARLY && tau > 0) {
+#pragma unroll
+      for (int c = 0; c < kLagChunks; ++c) {
+        const v4f *lr = (const v4f *)&tab_g->lag[kXaLag - 1 - 64 * c - ln][0];
+        lg[2 * c] = lr[0];
+        lg[2 * c + 1] = lr[1];
+      }
+    }
+    if (!XA_SPREAD && next_fast) {
+#pragma unroll
+      for (int q = 0; q < XA_PF; ++q) pf[q] = pnext[FLIP ? -64 * q : 64 * q];
+    }
+    issue_group(5);
+    XA_STAMP(4);
+    v2f h_ss = splat(0.f);  // backward steady input (last tile only)
+    if (last) {
+      // f = N v explicitly for s in [e-16, e-1] (clamped at e-1 beyond), one value per
+      // lane 0..15; h at the odd j in (e-17, e-1] in the unmerged form, one per lane 0..7
+      auto v_at = [&](int p) -> v2f {
+        const int r = p - base;
+        return r < 0 ? vcarry[64 + r] : buf[((r >> 5) - la) * kRow + (r & 31)];
+      };
+      v2f *fbuf = buf + 2 * kRow, *tbuf = buf + 3 * kRow;
+      if (ln < 16) {
+        CT tb = fresh(tab);
+        v2f acc = splat(0.f);
+        for (int i = 0; i < 9; ++i) acc = vfma(splat(tb->n9[i]), v_at(e - 16 + ln - i), acc);
+        fbuf[ln] = acc;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const v2f fe = fbuf[15];
+      h_ss = fe * fresh(tab)->mp_sum;
+      const int j0 = (e - 16) | 1;  // first odd position above e-17
+      if (ln < 8 && j0 + 2 * ln <= e - 1) {
+        CT tb = fresh(tab);
+        const int j = j0 + 2 * ln;
+        v2f acc = splat(0.f);
+        for (int t = 0; t < 17; ++t) {
+          const int sidx = j + t - (e - 16);
+          acc = vfma(splat(tb->mp17[t]), sidx < 16 ? fbuf[sidx] : fe, acc);
+        }
+        tbuf[ln] = acc;
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < kXaK; ++k) {
+        const int j = base + 32 * ln - 15 + 2 * k;
+        if (j > e - 1) h[k] = h_ss;
+        else if (j > e - 17) h[k] = tbuf[(j - j0) >> 1];
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    XA_STAMP(5);
+
+    // ---- backward all-pole cascade on h, descending (ln 63 holds the tile top):
+    //      pass 1, scan down, pass 2 from the exact entering state ----
+    Md q_exit;
+    {
+      Md qe;
+      {
+        Md m;
+        {
+          float a1[4], a2[4];
+          load_ap<1>(tab, a1, a2);
+          v2f s[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) s[r] = splat(0.f);
+#pragma unroll
+          for (int k = kXaK - 1; k >= 0; --k) (void)ap_step(h[k], s, a1, a2);
+          to_modal<1>(tab, s, m);
+        }
+        XA_STAMP(6);
+        issue_group(6);
+        Md qtop;  // state entering the tile from above: exact steady state on the last tile
+        {
+          CT tb = fresh(tab);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) qtop.r[r] = last ? tb->b.ss[r] * h_ss : splat(0.f);
+        }
+        if (last) fold_entering<1>(m, qtop, tab, ln == 63);
+        modal_scan<1, false>(m, tab, ln);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) qe.r[r] = wave_shift<kShl1>(qtop.r[r], m.r[r]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) q_exit.r[r] = lane_of(m.r[r], 0);
+      }
+      float a1[4], a2[4];
+      load_ap<1>(tab, a1, a2);
+      v2f s[8];
+      from_modal<1>(tab, qe, s);
+#pragma unroll
+      for (int k = kXaK - 1; k >= 0; --k) h[k] = ap_step(h[k], s, a1, a2);
+    }
+    XA_STAMP(7);
+    issue_group(7);
+    // ---- the tile below is complete: its top state is this tile's bottom state ----
+    if (tau > 0) {
+      if (!XA_LAG_EARLY) {
+#pragma unroll
+        for (int c = 0; c < kLagChunks; ++c) {
+          const v4f *lr = (const v4f *)&tab_g->lag[kXaLag - 1 - 64 * c - ln][0];
+          lg[2 * c] = lr[0];
+          lg[2 * c + 1] = lr[1];
+        }
+      }
+      finish_held(tau - 1, &q_exit, lg, ln);
+    }
+    XA_STAMP(8);
+    flush_tile(tau, h, ln);
+    XA_STAMP(9);
+  }
+  finish_held(nt - 1, nullptr, nullptr, lane);  // the last tile's top state was exact
+#if XA_STAMPS
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < kStampSegs; ++i) atomicAdd(&g_xa_stamps[i], st_acc[i]);
+    atomicAdd(&g_xa_stamps[kStampSegs], (unsigned long long)nt);
+  }
+#endif
+}
+
+template <bool MIX, int DT, int FLIP>
+static void xa_launch(const InDesc &in, int n, const float2 *lo, float2 *out, int frames,
+                      const XaTab *tab, hipStream_t st) {
+  hipLaunchKernelGGL((xa_stage_kernel<MIX, DT, FLIP>), dim3((unsigned)((frames + kWaves - 1) / kWaves)),
+                     dim3(64 * kWaves), 0, st, in, n, (const v2f *)lo, (v2f *)out, frames, tab);
+}
+
+}  // namespace xa
+
+#ifndef XA_STAMPS
+#define XA_STAMPS 0
+#endif
+// Debug hook (not part of zfft.h): copies and clears the stamp sums of a XA_STAMPS build
+// (segment cycles summed over waves, then the tile count); -1 in a normal build.
+extern "C" int zfft_debug_xa_stamps(unsigned long long *out) {
+#if XA_STAMPS
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(xa::g_xa_stamps), sizeof(xa::g_xa_stamps)) != hipSuccess) return -2;
+  unsigned long long z[xa::kStampSegs + 1] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(xa::g_xa_stamps), z, sizeof(z)) == hipSuccess ? 0 : -2;
+#else
+  (void)out;
+  return -1;
+#endif
+}
+
+hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix, float2 *out,
+                           int frames, const XaTab *tab, hipStream_t st) {
+  using namespace xa;
+  if (!mix) {
+    if (in.dtype != kInC64 || in.flip) return hipErrorInvalidValue;  // stages >= 1: internal
+    xa_launch<false, kInC64, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInC64) {
+    if (in.flip) xa_launch<true, kInC64, 1>(in, n, lo, out, frames, tab, st);
+    else xa_launch<true, kInC64, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInC32H) {
+    if (in.flip) xa_launch<true, kInC32H, 1>(in, n, lo, out, frames, tab, st);
+    else xa_launch<true, kInC32H, 0>(in, n, lo, out, frames, tab, st);
+  } else {
+    if (in.flip) xa_launch<true, kInCU8, 1>(in, n, lo, out, frames, tab, st);
+    else xa_launch<true, kInCU8, 0>(in, n, lo, out, frames, tab, st);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace zfft

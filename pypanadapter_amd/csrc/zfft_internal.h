@@ -92,6 +92,43 @@ struct XtModal {
 hipError_t launch_xt_stage(const InDesc &in, int n, const float2 *lo, bool mix,
                            float2 *out, int frames, const XtModal *tab, hipStream_t st);
 
+// "XA" decimation stage (xa_kernels.hip; design model tools/xa_proto.py).  The cascade
+// H = N(z)/D(z), N = b0 (1+z^-1)^8, is run as a forward all-pole cascade 1/D(z) at the
+// input rate, a 25-tap FIR M = N(z) N(1/z) D(-1/z) evaluated only at the kept (odd)
+// positions, and a backward all-pole cascade 1/D2(w), D2(z^2) = D(z) D(-z), at the output
+// rate: 8 + 12.5 + 4 multiply-adds per input sample instead of 2 x 17 for two DF2T passes,
+// with scipy's pad / steady-state edge rules carried over exactly.  One wave per frame,
+// tiles of 64 lanes x kXaB samples, states scanned over lanes in the real modal basis of
+// each all-pole cascade (sections slowest pole first, the lower-error order in fp32).
+constexpr int kXaB = 32;             // forward samples per lane and tile
+constexpr int kXaT = 64 * kXaB;      // tile (forward samples)
+constexpr int kXaK = kXaB / 2;       // kept outputs per lane and tile
+constexpr int kXaLag = 192;          // held-tile outputs corrected by the one-tile lag
+// scan levels per mode (modes follow the cascade order, slowest pole first): mode j needs
+// |lambda_j|^(S 2^levels) < 1e-9; checked when the tables are built
+constexpr int kXaLevels[4] = {4, 2, 1, 1};
+struct XaPass {                      // one all-pole cascade, DF-I state (y[t-1], y[t-2]) per section
+  float a1[4], a2[4];                // y = x - a1 y[t-1] - a2 y[t-2], cascade order
+  float ti[8][8];                    // T^-1: state -> real modal (block lower triangular)
+  float t[8][8];                     // T: real modal -> state (block lower triangular)
+  float ss[8];                       // modal steady state per unit constant input
+  float pS[4][2];                    // lambda_j^S (one lane sub-block of S steps)
+  float scan[4][4][2];               // lambda_j^(S 2^d), scan level d
+};
+struct XaTab {
+  XaPass f, b;                       // forward (full rate, S = kXaB), backward (S = kXaK)
+  float m25[25];                     // M on v[j-8 .. j+16]
+  float mp17[17];                    // N(1/z) D(-1/z) on f[j .. j+16] (frame-end form)
+  float n9[9];                       // N on v[s .. s-8] (f = N v, frame-end form)
+  float mp_sum;                      // h per unit constant f (backward steady input)
+  float vss;                         // forward cascade output per unit constant input
+  float pad_[2];
+  float lag[kXaLag][8];              // backward C A2^d T: held output d steps below the top
+};
+
+hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix,
+                           float2 *out, int frames, const XaTab *tab, hipStream_t st);
+
 struct WelchGeom {
   int n_fft, log2n;
   int n_win;

@@ -177,6 +177,169 @@ void xt_build_tables(XtModal &X) {
   }
 }
 
+
+// ---- XA tables (xa_kernels.hip, tools/xa_proto.py): all-pole cascades in DF-I state
+// (y_k[t-1], y_k[t-2]) per section, real modal bases, the 25-tap FIR and frame-end forms ----
+struct ApD {
+  double a1[4], a2[4];
+};
+void ap_step_d(const ApD &c, const double in[8], double u, double out[8], double *y) {
+  double s[8];
+  for (int i = 0; i < 8; ++i) s[i] = in[i];
+  double x = u;
+  for (int k = 0; k < 4; ++k) {
+    const double yy = x - c.a1[k] * s[2 * k] - c.a2[k] * s[2 * k + 1];
+    s[2 * k + 1] = s[2 * k];
+    s[2 * k] = yy;
+    x = yy;
+  }
+  for (int i = 0; i < 8; ++i) out[i] = s[i];
+  *y = x;
+}
+
+// Real modal basis of a cascade state matrix A (block lower triangular): mode j = the pole
+// pair of section j, eigenvector zero on sections < j, forward substitution below.
+void modal_basis(const Mat8 &A, const cd lam[4], Mat8 &T) {
+  T.assign(64, 0.0);
+  for (int j = 0; j < 4; ++j) {
+    cd v[8] = {};
+    const double p = A[(2 * j) * 8 + 2 * j], q = A[(2 * j) * 8 + 2 * j + 1];
+    v[2 * j] = q;
+    v[2 * j + 1] = lam[j] - p;
+    for (int k = j + 1; k < 4; ++k) {
+      cd r0 = 0, r1 = 0;
+      for (int l = 2 * j; l < 2 * k; ++l) {
+        r0 -= A[(2 * k) * 8 + l] * v[l];
+        r1 -= A[(2 * k + 1) * 8 + l] * v[l];
+      }
+      const cd m00 = A[(2 * k) * 8 + 2 * k] - lam[j], m01 = A[(2 * k) * 8 + 2 * k + 1];
+      const cd m10 = A[(2 * k + 1) * 8 + 2 * k], m11 = A[(2 * k + 1) * 8 + 2 * k + 1] - lam[j];
+      const cd det = m00 * m11 - m01 * m10;
+      v[2 * k] = (r0 * m11 - m01 * r1) / det;
+      v[2 * k + 1] = (m00 * r1 - m10 * r0) / det;
+    }
+    double nrm = 0;
+    int big = 0;
+    for (int i = 0; i < 8; ++i) {
+      nrm += std::norm(v[i]);
+      if (std::abs(v[i]) > std::abs(v[big])) big = i;
+    }
+    const cd rot = std::conj(v[big]) / std::abs(v[big]) / std::sqrt(nrm);
+    for (int i = 0; i < 8; ++i) {
+      const cd w = v[i] * rot;
+      T[i * 8 + 2 * j] = w.real();
+      T[i * 8 + 2 * j + 1] = w.imag();
+    }
+  }
+}
+
+// One pass: fills P, the output table cm (steps rows) and, when lag != nullptr, the
+// far-field rows C A^d T for d < n_lag.
+bool xa_pass_tables(const ApD &c, int steps, XaPass &P, float (*lag)[8], int n_lag) {
+  Mat8 A(64);
+  double C[8];
+  for (int q = 0; q < 8; ++q) {
+    double e[8] = {0}, s2[8], y;
+    e[q] = 1.0;
+    ap_step_d(c, e, 0.0, s2, &y);
+    for (int r = 0; r < 8; ++r) A[r * 8 + q] = s2[r];
+    C[q] = y;
+  }
+  cd lam[4];
+  for (int j = 0; j < 4; ++j) lam[j] = cd(-0.5 * c.a1[j], std::sqrt(c.a2[j] - 0.25 * c.a1[j] * c.a1[j]));
+  Mat8 T, Ti;
+  modal_basis(A, lam, T);
+  mat_inverse8(T, Ti);
+  double st[8], x = 1.0;
+  for (int k = 0; k < 4; ++k) {
+    P.a1[k] = (float)c.a1[k];
+    P.a2[k] = (float)c.a2[k];
+    x /= 1.0 + c.a1[k] + c.a2[k];
+    st[2 * k] = st[2 * k + 1] = x;
+  }
+  for (int r = 0; r < 8; ++r) {
+    double acc = 0;
+    for (int k = 0; k < 8; ++k) acc += Ti[r * 8 + k] * st[k];
+    P.ss[r] = (float)acc;
+    for (int k = 0; k < 8; ++k) {
+      P.ti[r][k] = (float)Ti[r * 8 + k];
+      P.t[r][k] = (float)T[r * 8 + k];
+    }
+  }
+  for (int j = 0; j < 4; ++j) {
+    // the kernel's truncated scan must reach fp32-negligible powers for every mode
+    if (std::pow(std::abs(lam[j]), (double)(steps << kXaLevels[j])) > 1e-9) return false;
+    const cd w = std::pow(lam[j], steps);
+    P.pS[j][0] = (float)w.real();
+    P.pS[j][1] = (float)w.imag();
+    for (int d = 0; d < 4; ++d) {
+      const cd u = std::pow(lam[j], steps << d);
+      P.scan[d][j][0] = (float)u.real();
+      P.scan[d][j][1] = (float)u.imag();
+    }
+  }
+  Mat8 AtT = T;  // A^t T
+  for (int t = 0; lag && t < n_lag; ++t) {
+    for (int q = 0; q < 8; ++q) {
+      double acc = 0;
+      for (int r = 0; r < 8; ++r) acc += C[r] * AtT[r * 8 + q];
+      lag[t][q] = (float)acc;
+    }
+    AtT = matmul8(A, AtT);
+  }
+  return true;
+}
+
+bool xa_build_tables(XaTab &X) {
+  // sections slowest pole first (the lower-error fp32 order; any order is exact)
+  ApD fw, bw;
+  for (int k = 0; k < 4; ++k) {
+    const double a1 = kDecimSos[3 - k][4], a2 = kDecimSos[3 - k][5];
+    fw.a1[k] = a1;
+    fw.a2[k] = a2;
+    bw.a1[k] = 2.0 * a2 - a1 * a1;  // D(z) D(-z) = D2(z^2)
+    bw.a2[k] = a2 * a2;
+  }
+  if (!xa_pass_tables(fw, kXaB, X.f, nullptr, 0) || !xa_pass_tables(bw, kXaK, X.b, X.lag, kXaLag))
+    return false;
+  // N = b0 (1 + z^-1)^8 (sections 1..3 are exactly [1, 2, 1], section 0 is b0 [1, 2, 1])
+  double n9[9], dneg[9] = {1.0}, mp[17] = {0}, m25[25] = {0};
+  const double b0 = kDecimSos[0][0];
+  for (int i = 0; i < 9; ++i) {
+    double bin = 1.0;
+    for (int r = 0; r < i; ++r) bin = bin * (8 - r) / (r + 1);
+    n9[i] = b0 * bin;
+  }
+  int len = 1;
+  for (int k = 0; k < 4; ++k) {  // D(-z) = prod (1 - a1 z^-1 + a2 z^-2)
+    const double c1 = -kDecimSos[k][4], c2 = kDecimSos[k][5];
+    double nx[9] = {0};
+    for (int i = 0; i < len; ++i) {
+      nx[i] += dneg[i];
+      nx[i + 1] += c1 * dneg[i];
+      nx[i + 2] += c2 * dneg[i];
+    }
+    len += 2;
+    for (int i = 0; i < len; ++i) dneg[i] = nx[i];
+  }
+  for (int i = 0; i < 9; ++i)
+    for (int k = 0; k < 9; ++k) mp[i + k] += n9[i] * dneg[k];   // taps on f[j + t]
+  for (int t = 0; t < 17; ++t)
+    for (int i = 0; i < 9; ++i) m25[t + i] += mp[t] * n9[8 - i];  // taps on v[j - 8 + u]
+  double mps = 0, vss = 1.0;
+  for (int t = 0; t < 17; ++t) {
+    X.mp17[t] = (float)mp[t];
+    mps += mp[t];
+  }
+  for (int u = 0; u < 25; ++u) X.m25[u] = (float)m25[u];
+  for (int i = 0; i < 9; ++i) X.n9[i] = (float)n9[i];
+  for (int k = 0; k < 4; ++k) vss /= 1.0 + fw.a1[k] + fw.a2[k];
+  X.mp_sum = (float)mps;
+  X.vss = (float)vss;
+  X.pad_[0] = X.pad_[1] = 0.f;
+  return true;
+}
+
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -238,9 +401,10 @@ struct zfft_plan {
   std::vector<std::string> mark_names;
   std::string names_buf;
   int n_marks = 0;
-  int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows, 3 exact tiles
+  int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows, 3 exact tiles,
+                // 4 XA tiles (all-pole + FIR + half-rate all-pole)
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
-  DevBuf edge, xk, xt_tab, tws, means, z4;
+  DevBuf edge, xk, xt_tab, xa_tab, tws, means, z4;
 };
 
 namespace {
@@ -498,12 +662,34 @@ int run_xt(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t
   return ZFFT_OK;
 }
 
+
+// XA path: one kernel per stage, one wave per frame, stage outputs natural layout.
+int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t> &n,
+           const float2 **out, hipStream_t st) {
+  hipError_t e = p->ping.ensure((size_t)frames * n[1] * sizeof(float2));
+  if (e == hipSuccess && p->K > 1) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+  const float2 *cur = nullptr;
+  for (int k = 0; k < p->K; ++k) {
+    float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
+    const InDesc src = k == 0 ? in : InDesc{cur, n[k], n[k], kInC64, 0};
+    e = launch_xa_stage(src, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
+                        p->xa_tab.as<XaTab>(), st);
+    if (e != hipSuccess) return hip_fail(e, "xa_stage launch");
+    mark(p, st, k == 0 ? "xa_stage_mix" : "xa_stage");
+    cur = dst;
+  }
+  *out = cur;
+  return ZFFT_OK;
+}
+
 int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
                   const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   int rc = ensure_lo(p, L);
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
+  if (p->path == 4) return run_xa(p, in, frames, n, out, st);
   if (p->path == 3 || (p->path == 0 && frames >= kXtMinFrames))
     return run_xt(p, in, frames, n, out, st);
   if (use_fused(p, L)) return run_fused(p, in, L, frames, n, out, st);
@@ -682,6 +868,16 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
     e = p->xt_tab.ensure(sizeof(XtModal));
     if (e == hipSuccess) e = hipMemcpy(p->xt_tab.p, &xt, sizeof(XtModal), hipMemcpyHostToDevice);
   }
+  if (e == hipSuccess) {
+    static XaTab xa{};
+    static const bool xa_ok = xa_build_tables(xa);
+    if (!xa_ok) {
+      zfft_plan_destroy(p);
+      return fail(ZFFT_EHIP, "XA tables: scan levels too shallow for the filter poles");
+    }
+    e = p->xa_tab.ensure(sizeof(XaTab));
+    if (e == hipSuccess) e = hipMemcpy(p->xa_tab.p, &xa, sizeof(XaTab), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     zfft_plan_destroy(p);
     return hip_fail(e, "twiddle upload");
@@ -695,7 +891,7 @@ int zfft_plan_destroy(zfft_plan *p) {
   (void)hipSetDevice(p->cfg.device);
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->yf, &p->ping, &p->pong, &p->rows,
-                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xt_tab,
+                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xt_tab, &p->xa_tab,
                     &p->tws, &p->means, &p->z4})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
@@ -720,8 +916,9 @@ int zfft_plan_timing(zfft_plan *p, int32_t enable) {
 }
 
 int zfft_plan_path(zfft_plan *p, int32_t path) {
-  if (!p || path < 0 || path > 3)
-    return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused) or 3 (exact tiles)");
+  if (!p || path < 0 || path > 4)
+    return fail(ZFFT_EINVAL,
+                "path must be 0 (auto), 1 (exact), 2 (fused), 3 (exact tiles) or 4 (XA tiles)");
   p->path = path;
   return ZFFT_OK;
 }

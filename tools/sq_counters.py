@@ -13,7 +13,7 @@ acc = defaultdict(lambda: defaultdict(float))
 cnt = defaultdict(lambda: defaultdict(int))
 for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        m = re.search(r"zfft::([a-z_0-9]+)(<[^>(]*>)?", r["Kernel_Name"])
+        m = re.search(r"zfft::(?:xa::)?([a-z_0-9]+)(<[^>(]*>)?", r["Kernel_Name"])
         if not m:
             continue
         k = m.group(1) + (m.group(2) or "")
