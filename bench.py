@@ -127,7 +127,8 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="frames per rank (default: config)")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--warm", type=int, default=0)
-    ap.add_argument("--path", type=int, default=0, help="0 auto, 1 exact order, 2 fused interior")
+    ap.add_argument("--path", type=int, default=0,
+                    help="0 auto, 1 exact order, 2 fused interior, 3 DF2T exact tiles, 4 XA tiles")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")

@@ -63,14 +63,15 @@ constexpr int kWaves = 2;               // waves (frames) per workgroup
 #endif
 
 typedef float v4f __attribute__((ext_vector_type(4)));
-// The filter tables live in LDS (one copy per workgroup, uniform-address broadcast reads
-// into VGPRs, pipelined by the compiler): as scalar K$ reads they cost ~150 s_load +
-// lgkmcnt waits per tile, the largest stall of the loop.  The far-field `lag` rows stay
-// in global memory (per-lane rows).
-typedef const XaTab __attribute__((address_space(3))) *CT;
-constexpr int kTabWords = (int)(offsetof(XaTab, lag) / sizeof(float) + 3) / 4 * 4;
+// LDS pointers keep their address space (a generic pointer turns every LDS access into a
+// flat access, which waits on vector memory too)
+typedef v2f __attribute__((address_space(3))) *LP;
+typedef v4f __attribute__((address_space(3))) *LP4;
+// Filter tables: scalar (K$) reads of the constant table; the far-field `lag` rows are
+// per-lane vector reads.
+typedef const XaTab __attribute__((address_space(4))) *CT;
 // an opaque copy per phase: reads are not hoisted out of the tile loop (which would pin
-// ~100 table values in VGPRs), each phase re-reads the few it needs
+// the whole table in SGPRs and spill), each phase re-reads the few it needs
 typedef const XaTab __attribute__((address_space(4))) *CS;  // scalar reads (global copy)
 __device__ __forceinline__ CS fresh_s(CS p) {
   asm volatile("" : "+s"(p));
@@ -141,7 +142,7 @@ __device__ __forceinline__ v2f ap_step(v2f x, v2f s[8], const float a1[4], const
 }
 
 template <int PASS>  // 0 forward, 1 backward
-__device__ __forceinline__ const XaPass __attribute__((address_space(3))) &pass_of(CT t) {
+__device__ __forceinline__ const XaPass __attribute__((address_space(4))) &pass_of(CT t) {
   if constexpr (PASS == 0) return t->f;
   else return t->b;
 }
@@ -252,20 +253,16 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
                                                                         v2f *__restrict__ out, int frames,
                                                                         const XaTab *tab_g) {
   __shared__ __attribute__((aligned(16))) v2f lds_all[kWaves][kBuf];
-  __shared__ __attribute__((aligned(16))) float ltab[kTabWords];
-  for (int i = threadIdx.x; i < kTabWords / 4; i += 64 * kWaves)
-    ((v4f *)ltab)[i] = ((const v4f *)tab_g)[i];
-  __syncthreads();
-  const CT tab = (CT)(const XaTab __attribute__((address_space(3))) *)ltab;
+  const CT tab = (CT)tab_g;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR
   const int f = blockIdx.x * kWaves + wv;
   if (f >= frames) return;  // whole wave
-  v2f *const buf0 = lds_all[wv];            // half-tile transposes: 32 rows of kRow v2f
-  v2f *buf = buf0;
-  v2f *pcarry = buf + kHalfRows * kRow;     // lane 63's FIR neighbour part, for next lane 0
-  v2f *vcarry = pcarry + 16;                // rows 62, 63 of the tile before the last
-  v2f *cq = vcarry + 64;                    // lo at the 32 chunk starts of the tile
+  const LP buf0 = (LP)lds_all[wv];           // half-tile transposes: 32 rows of kRow v2f
+  LP buf = buf0;
+  LP pcarry = buf + kHalfRows * kRow;       // lane 63's FIR neighbour part, for next lane 0
+  LP vcarry = pcarry + 16;                  // rows 62, 63 of the tile before the last
+  LP cq = vcarry + 64;                      // lo at the 32 chunk starts of the tile
   const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
   const int nt = (e + 15) / kXaT + 1;  // the last FIR/backward tile reaches e - 1
   v2f *__restrict__ o = out + (int64_t)f * n_out;
@@ -314,13 +311,13 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       if ((ln >> 5) == hf) {  // lanes of this half: 16 outputs each into row ln % 32
-        v4f *hw = (v4f *)(buf + (ln & 31) * kHeldRow);
+        LP4 hw = (LP4)(buf + (ln & 31) * kHeldRow);
 #pragma unroll
         for (int k = 0; k < kXaK / 2; ++k) hw[k] = v4f{h[2 * k].x, h[2 * k].y, h[2 * k + 1].x, h[2 * k + 1].y};
       }
       __builtin_amdgcn_wave_barrier();
       // output idx = 64 c + ln (c in this half) sits at row idx/16 - 32 hf, column ln % 16
-      const v2f *hr = buf + (ln >> 4) * kHeldRow + (ln & 15);
+      const LP hr = buf + (ln >> 4) * kHeldRow + (ln & 15);
 #pragma unroll
       for (int cc = 0; cc < kChunks / 2; ++cc) {
         const int c = hf * (kChunks / 2) + cc;
@@ -386,7 +383,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     int ln = lane;
     asm volatile("" : "+v"(ln));
     {  // opaque per-tile copy of the LDS base, for the same reason
-      v2f *b = buf0;
+      LP b = buf0;
       asm volatile("" : "+s"(b));
       buf = b;
       pcarry = buf + kHalfRows * kRow;
@@ -398,17 +395,19 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     v2f y[kXaB];
     {
       const bool fast = fast_tile(base);  // wave-uniform
-      if (fast && XA_PF < kXaB) {
-        const int i0 = base - kPad + ln;
-        const RawT *p = src + (FLIP ? in.len - 1 - i0 : i0);
+      // chunks not loaded a tile ahead: the first half now, the second half as soon as
+      // the first is in LDS (32 raw VGPRs in flight at a time)
+      const int i0 = base - kPad + ln;
+      const RawT *pcur = src + (FLIP ? in.len - 1 - i0 : i0);
+      if (fast && XA_PF < kXaB / 2) {
 #pragma unroll
-        for (int q = XA_PF; q < kXaB; ++q) pf[q] = p[FLIP ? -64 * q : 64 * q];
+        for (int q = XA_PF; q < kXaB / 2; ++q) pf[q] = pcur[FLIP ? -64 * q : 64 * q];
       }
       if (MIX && fast) {
         if (ln < 32) cq[ln] = cqv;
         __builtin_amdgcn_wave_barrier();
       }
-      v2f *st = buf + (ln >> 5) * kRow + (ln & 31);
+      LP st = buf + (ln >> 5) * kRow + (ln & 31);
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         if (fast) {
@@ -419,13 +418,18 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
             if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl));
             st[2 * kRow * qq] = x;
           }
+          if (hf == 0 && XA_PF < kXaB) {
+            __builtin_amdgcn_sched_barrier(0);  // keep these loads behind the first half's use
+#pragma unroll
+            for (int q = (XA_PF > kXaB / 2 ? XA_PF : kXaB / 2); q < kXaB; ++q) pf[q] = pcur[FLIP ? -64 * q : 64 * q];
+          }
         } else {
 #pragma unroll 4
           for (int qq = 0; qq < kXaB / 2; ++qq) st[2 * kRow * qq] = ext(base + ln + 64 * (hf * (kXaB / 2) + qq));
         }
         __builtin_amdgcn_wave_barrier();
         if ((ln >> 5) == hf) {
-          const v4f *rp = (const v4f *)(buf + (ln & 31) * kRow);
+          const LP4 rp = (LP4)(buf + (ln & 31) * kRow);
 #pragma unroll
           for (int t = 0; t < kXaB / 2; ++t) {
             const v4f w = rp[t];
@@ -518,7 +522,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         }
       }
       {  // neighbour shares: ln i takes ln i-1's P, ln 0 the previous tile's ln 63's
-        const v4f *pc = (const v4f *)pcarry;
+        const LP4 pc = (LP4)pcarry;
 #pragma unroll
         for (int k2 = 0; k2 < 6; ++k2) {
           const v4f c4 = pc[k2];
@@ -527,7 +531,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         }
         __builtin_amdgcn_wave_barrier();
         if (ln == 63) {
-          v4f *pw = (v4f *)pcarry;
+          LP4 pw = (LP4)pcarry;
 #pragma unroll
           for (int k2 = 0; k2 < 6; ++k2) pw[k2] = v4f{P[2 * k2].x, P[2 * k2].y, P[2 * k2 + 1].x, P[2 * k2 + 1].y};
         }
@@ -539,11 +543,19 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     // addresses of these once-per-frame paths are not hoisted out of the loop.)
     const int la = max(0, (e - 25 - base) >> 5);
     if (tau >= nt - 2) {
-      v2f *dst = nullptr;
-      if (!last && ln >= 62) dst = vcarry + (ln - 62) * 32;
-      if (last && (ln == la || ln == la + 1)) dst = buf + (ln - la) * kRow;
-      if (dst != nullptr) {
-        v4f *wp = (v4f *)dst;
+      // (no null test on an LDS pointer: LDS address 0 is this workgroup's first row)
+      LP dst = buf;
+      bool put = false;
+      if (!last && ln >= 62) {
+        dst = vcarry + (ln - 62) * 32;
+        put = true;
+      }
+      if (last && (ln == la || ln == la + 1)) {
+        dst = buf + (ln - la) * kRow;
+        put = true;
+      }
+      if (put) {
+        LP4 wp = (LP4)dst;
 #pragma unroll
         for (int t = 0; t < kXaB / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
       }
@@ -574,7 +586,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         const int r = p - base;
         return r < 0 ? vcarry[64 + r] : buf[((r >> 5) - la) * kRow + (r & 31)];
       };
-      v2f *fbuf = buf + 2 * kRow, *tbuf = buf + 3 * kRow;
+      LP fbuf = buf + 2 * kRow, tbuf = buf + 3 * kRow;
       if (ln < 16) {
         CT tb = fresh(tab);
         v2f acc = splat(0.f);

@@ -689,9 +689,9 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  if (p->path == 4) return run_xa(p, in, frames, n, out, st);
-  if (p->path == 3 || (p->path == 0 && frames >= kXtMinFrames))
-    return run_xt(p, in, frames, n, out, st);
+  if (p->path == 4 || (p->path == 0 && frames >= kXtMinFrames))
+    return run_xa(p, in, frames, n, out, st);
+  if (p->path == 3) return run_xt(p, in, frames, n, out, st);
   if (use_fused(p, L)) return run_fused(p, in, L, frames, n, out, st);
   return run_exact(p, in, p->lo.as<float2>(), frames, n, out, st);
 }
