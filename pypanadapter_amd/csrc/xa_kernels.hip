@@ -58,6 +58,13 @@ constexpr int kWaves = 2;               // waves (frames) per workgroup
 #ifndef XA_SPREAD
 #define XA_SPREAD 1                     // next-tile loads in 8 groups spread over the tile
 #endif
+// diagnostic builds only (results invalid): no stage-output stores / one shared input frame
+#ifndef XA_DIAG_NOSTORE
+#define XA_DIAG_NOSTORE 0
+#endif
+#ifndef XA_DIAG_ONEFRAME
+#define XA_DIAG_ONEFRAME 0
+#endif
 #ifndef XA_LAG_EARLY
 #define XA_LAG_EARLY 1                  // lag rows loaded before the backward pass
 #endif
@@ -325,7 +332,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         if (c >= kChunks - kLagChunks) {
           held[c - (kChunks - kLagChunks)] = v;
         } else if (inside || (m0 + 64 * c >= 0 && m0 + 64 * c < n_out)) {
-          od[64 * c] = v;
+          if (!XA_DIAG_NOSTORE) od[64 * c] = v;
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -348,14 +355,15 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         v = vfma(splat(l1.w), q->r[7], v);
       }
       const int m = m0 + 64 * c;
-      if (m >= 0 && m < n_out) o[m] = v;
+      if (m >= 0 && m < n_out && !XA_DIAG_NOSTORE) o[m] = v;
     }
   };
 
   // coalesced tile loads: sample s = 64 q + lane of the tile -> row s/32, in two halves; a
   // fast tile (inside [27, n + 27): no odd extension) is loaded during the previous tile
   typedef typename Raw<DT>::T RawT;
-  const RawT *__restrict__ src = (const RawT *)in.p + (int64_t)f * in.stride;
+  // (XA_DIAG_ONEFRAME: every wave reads frame 0, an L2/MALL-resident input -- diagnostic)
+  const RawT *__restrict__ src = (const RawT *)in.p + (XA_DIAG_ONEFRAME ? 0 : (int64_t)f * in.stride);
   auto fast_tile = [&](int b) { return b >= kPad && b + kXaT <= n + kPad; };
   v2f wl = splat(0.f);  // lo[n0 + l] = lo[n0] w^l: w^l = lo[l] / sqrt(2), per lane
   if constexpr (MIX) wl = lo[lane] * 0.70710678118654752f;
@@ -503,8 +511,13 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         for (int t = 0; t < 25; ++t) m25s[t] = tbs->m25[t];
 #pragma unroll
         for (int t = 0; t < kXaB; ++t) {
-          if (t == 11) issue_group(3);
-          if (t == 22) issue_group(4);
+          // the rest of the next tile's loads go out during pass 2, ahead of the lag rows
+          // (finish_held waits on those; vmcnt counts in issue order)
+          if (t == 4) issue_group(3);
+          if (t == 10) issue_group(4);
+          if (t == 16) issue_group(5);
+          if (t == 22) issue_group(6);
+          if (t == 28) issue_group(7);
           const v2f v = ap_step(y[t], s, a1, a2);
           y[t] = v;
 #pragma unroll
@@ -512,12 +525,15 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
             const int tap = 24 + t - 1 - 2 * k;
             if (tap >= 0 && tap < 25) h[k] = vfma(splat(m25s[tap]), v, h[k]);
           }
-          if (t >= 9) {
+        }
+        // this lane's share of its right neighbour's outputs: W[m] = v[8 + m], 1 <= m < 24
+        // (after pass 2, so the pass's state registers are free)
 #pragma unroll
-            for (int k = 0; k < 12; ++k) {
-              const int tap = t - 8 - 1 - 2 * k;
-              if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), v, P[k]);
-            }
+        for (int t = 9; t < kXaB; ++t) {
+#pragma unroll
+          for (int k = 0; k < 12; ++k) {
+            const int tap = t - 8 - 1 - 2 * k;
+            if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), y[t], P[k]);
           }
         }
       }
@@ -576,7 +592,6 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
 #pragma unroll
       for (int q = 0; q < XA_PF; ++q) pf[q] = pnext[FLIP ? -64 * q : 64 * q];
     }
-    issue_group(5);
     XA_STAMP(4);
     v2f h_ss = splat(0.f);  // backward steady input (last tile only)
     if (last) {
@@ -636,7 +651,6 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
           to_modal<1>(tab, s, m);
         }
         XA_STAMP(6);
-        issue_group(6);
         Md qtop;  // state entering the tile from above: exact steady state on the last tile
         {
           CT tb = fresh(tab);
@@ -658,7 +672,6 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
       for (int k = kXaK - 1; k >= 0; --k) h[k] = ap_step(h[k], s, a1, a2);
     }
     XA_STAMP(7);
-    issue_group(7);
     // ---- the tile below is complete: its top state is this tile's bottom state ----
     if (tau > 0) {
       if (!XA_LAG_EARLY) {
