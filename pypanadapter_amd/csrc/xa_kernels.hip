@@ -65,6 +65,9 @@ constexpr int kWaves = 2;               // waves (frames) per workgroup
 #ifndef XA_DIAG_ONEFRAME
 #define XA_DIAG_ONEFRAME 0
 #endif
+#ifndef XA_LAG_LDS
+#define XA_LAG_LDS 1                    // lag rows copied to LDS once per workgroup
+#endif
 #ifndef XA_LAG_EARLY
 #define XA_LAG_EARLY 1                  // lag rows loaded before the backward pass
 #endif
@@ -261,6 +264,11 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
                                                                         const XaTab *tab_g) {
   __shared__ __attribute__((aligned(16))) v2f lds_all[kWaves][kBuf];
   const CT tab = (CT)tab_g;
+#if XA_LAG_LDS
+  __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];
+  for (int i = threadIdx.x; i < kXaLag * 2; i += 64 * kWaves) lag_l[i] = ((const v4f *)tab_g->lag)[i];
+  __syncthreads();
+#endif
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR
   const int f = blockIdx.x * kWaves + wv;
@@ -580,7 +588,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     // lag rows for the held tile's top outputs, then the next tile's loads: both land
     // while the backward pass runs
     v4f lg[2 * kLagChunks];
-    if (XA_LAG_EARLY && tau > 0) {
+    if (!XA_LAG_LDS && XA_LAG_EARLY && tau > 0) {
 #pragma unroll
       for (int c = 0; c < kLagChunks; ++c) {
         const v4f *lr = (const v4f *)&tab_g->lag[kXaLag - 1 - 64 * c - ln][0];
@@ -674,6 +682,14 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     XA_STAMP(7);
     // ---- the tile below is complete: its top state is this tile's bottom state ----
     if (tau > 0) {
+#if XA_LAG_LDS
+#pragma unroll
+      for (int c = 0; c < kLagChunks; ++c) {
+        const int d = kXaLag - 1 - 64 * c - ln;
+        lg[2 * c] = lag_l[2 * d];
+        lg[2 * c + 1] = lag_l[2 * d + 1];
+      }
+#else
       if (!XA_LAG_EARLY) {
 #pragma unroll
         for (int c = 0; c < kLagChunks; ++c) {
@@ -682,6 +698,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
           lg[2 * c + 1] = lr[1];
         }
       }
+#endif
       finish_held(tau - 1, &q_exit, lg, ln);
     }
     XA_STAMP(8);

@@ -22,7 +22,7 @@ from collections import defaultdict
 
 
 def kname(name: str) -> str:
-    m = re.search(r"zfft::([a-z_0-9]+)(<[^>(]*>)?", name)
+    m = re.search(r"zfft::(?:xa::)?([a-z_0-9]+)(<[^>(]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name[:60]
 
 
