@@ -376,7 +376,11 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
   v2f wl = splat(0.f);  // lo[n0 + l] = lo[n0] w^l: w^l = lo[l] / sqrt(2), per lane
   if constexpr (MIX) wl = lo[lane] * 0.70710678118654752f;
   v2f cqv = splat(0.f);  // lo[next tile start - 27 + 64 (lane % 32)], loaded a tile ahead
-  RawT pf[kXaB];  // [0, XA_PF): loaded a tile ahead; the rest at the tile start
+  // chunks [0, XA_PF) are loaded a tile ahead (loop-carried registers); the rest are loaded
+  // at the tile start into registers local to the iteration (so they are not carried, and
+  // not held, across the whole loop)
+  constexpr int kPfc = XA_PF > 0 ? XA_PF : 1;
+  RawT pf[kPfc];
   // next-tile loads: group g = chunks [4g, 4g + 4), issued at 8 points of the tile
   const RawT *pnext = src;
   bool next_fast = false;
@@ -385,7 +389,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + 64 * (lane & 31)];
     if (XA_SPREAD && next_fast && 4 * g < XA_PF) {
 #pragma unroll
-      for (int q = 4 * g; q < 4 * g + 4 && q < XA_PF; ++q) pf[q] = pnext[FLIP ? -64 * q : 64 * q];
+      for (int q = 4 * g; q < 4 * g + 4 && q < XA_PF; ++q) pf[q < kPfc ? q : 0] = pnext[FLIP ? -64 * q : 64 * q];
     }
   };
 
@@ -415,34 +419,8 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
       // the first is in LDS (32 raw VGPRs in flight at a time)
       const int i0 = base - kPad + ln;
       const RawT *pcur = src + (FLIP ? in.len - 1 - i0 : i0);
-      if (fast && XA_PF < kXaB / 2) {
-#pragma unroll
-        for (int q = XA_PF; q < kXaB / 2; ++q) pf[q] = pcur[FLIP ? -64 * q : 64 * q];
-      }
-      if (MIX && fast) {
-        if (ln < 32) cq[ln] = cqv;
-        __builtin_amdgcn_wave_barrier();
-      }
       LP st = buf + (ln >> 5) * kRow + (ln & 31);
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        if (fast) {
-#pragma unroll
-          for (int qq = 0; qq < kXaB / 2; ++qq) {
-            const int q = hf * (kXaB / 2) + qq;
-            v2f x = cvt_raw<DT>(pf[q]);
-            if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl));
-            st[2 * kRow * qq] = x;
-          }
-          if (hf == 0 && XA_PF < kXaB) {
-            __builtin_amdgcn_sched_barrier(0);  // keep these loads behind the first half's use
-#pragma unroll
-            for (int q = (XA_PF > kXaB / 2 ? XA_PF : kXaB / 2); q < kXaB; ++q) pf[q] = pcur[FLIP ? -64 * q : 64 * q];
-          }
-        } else {
-#pragma unroll 4
-          for (int qq = 0; qq < kXaB / 2; ++qq) st[2 * kRow * qq] = ext(base + ln + 64 * (hf * (kXaB / 2) + qq));
-        }
+      auto read_rows = [&](int hf) {  // lanes of half hf take their rows
         __builtin_amdgcn_wave_barrier();
         if ((ln >> 5) == hf) {
           const LP4 rp = (LP4)(buf + (ln & 31) * kRow);
@@ -454,6 +432,42 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
           }
         }
         __builtin_amdgcn_wave_barrier();
+      };
+      // the fast and the edge path are separate blocks end to end: raw registers of the
+      // fast path never live across the edge path's code (which would force their spill)
+      if (fast) {
+        RawT pl[kXaB - XA_PF > 0 ? kXaB - XA_PF : 1];
+        if (XA_PF < kXaB / 2) {
+#pragma unroll
+          for (int q = XA_PF; q < kXaB / 2; ++q) pl[q - XA_PF] = pcur[FLIP ? -64 * q : 64 * q];
+        }
+        if (MIX) {
+          if (ln < 32) cq[ln] = cqv;
+          __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+          for (int qq = 0; qq < kXaB / 2; ++qq) {
+            const int q = hf * (kXaB / 2) + qq;
+            v2f x = cvt_raw<DT>(q < XA_PF ? pf[q < kPfc ? q : 0] : pl[q >= XA_PF ? q - XA_PF : 0]);
+            if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl));
+            st[2 * kRow * qq] = x;
+          }
+          if (hf == 0 && XA_PF < kXaB) {
+            __builtin_amdgcn_sched_barrier(0);  // keep these loads behind the first half's use
+#pragma unroll
+            for (int q = (XA_PF > kXaB / 2 ? XA_PF : kXaB / 2); q < kXaB; ++q) pl[q - XA_PF] = pcur[FLIP ? -64 * q : 64 * q];
+          }
+          read_rows(hf);
+        }
+      } else {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll 4
+          for (int qq = 0; qq < kXaB / 2; ++qq) st[2 * kRow * qq] = ext(base + ln + 64 * (hf * (kXaB / 2) + qq));
+          read_rows(hf);
+        }
       }
     }
     next_fast = tau + 1 < nt && fast_tile(base + kXaT);  // wave-uniform
@@ -598,7 +612,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     }
     if (!XA_SPREAD && next_fast) {
 #pragma unroll
-      for (int q = 0; q < XA_PF; ++q) pf[q] = pnext[FLIP ? -64 * q : 64 * q];
+      for (int q = 0; q < XA_PF; ++q) pf[q < kPfc ? q : 0] = pnext[FLIP ? -64 * q : 64 * q];
     }
     XA_STAMP(4);
     v2f h_ss = splat(0.f);  // backward steady input (last tile only)
