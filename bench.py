@@ -228,12 +228,22 @@ def main():
     for i, (nm, ms) in enumerate(zip(names, launch_ms)):
         kernels[f"{i}:{nm}"] = round(ms, 4)
     dominant = max(kernels, key=lambda k: kernels[k]) if kernels else None
+    dom_roof = None
+    if dominant is not None and "stage_mix" in dominant:
+        # the stage-0 decimator: reads the caller's IQ (bps*L per frame), writes the first
+        # decimated stage (complex64, ceil(L/2) per frame)
+        dom_bytes = F * (bps * L + 8 * ((L + 1) // 2))
+        dom_gbs = dom_bytes / (kernels[dominant] / 1e3) / 1e9
+        dom_roof = {"kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes,
+                    "achieved": round(dom_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(dom_gbs / HBM_PEAK_GBS, 4), "launch_ms": kernels[dominant]}
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             if (tj.get("frames") == F and tj.get("in_dtype", "complex64") == args.in_dtype
+                    and tj.get("schedule") == "xa"  # measured on the current auto schedule
                     and not args.path and not args.block and not args.warm):
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
@@ -263,6 +273,7 @@ def main():
                      "event_ms_per_step": round(ev_ms_step, 4)},
         "kernels": kernels,
         "dominant_kernel": dominant,
+        "dominant_roofline": dom_roof,
         "rows_finite": finite,
         "cpu_baseline": cpu,
     }

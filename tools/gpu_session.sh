@@ -26,7 +26,7 @@ run() {  # name seconds cmd...
 for s in $STEPS; do
   case $s in
     tests)
-      run pytest_gpu 1100 python -m pytest tests -m gpu -q -p no:cacheprovider -rf
+      run pytest_gpu 1100 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --timeout 120 --timeout-method thread
       rc=$?
       [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     smoke)
@@ -59,7 +59,7 @@ for s in $STEPS; do
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
         -d "$OUT/pmc_write_$TAG" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu || exit $?
       python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG" 4096 cfg2 \
-        "$OUT/traffic_cfg2_$TAG.json" > /dev/null || exit $? ;;
+        "$OUT/traffic_cfg2_$TAG.json" xa > /dev/null || exit $? ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac

@@ -10,7 +10,7 @@ widths are uncalibrated; both raw and corrected sums are kept.
 Per step = (sum over every zfft dispatch) / (number of welch_rows dispatches): each
 process call launches welch_rows exactly once.
 
-usage: tools/pmc_traffic.py <fetch_dir> <write_dir> <frames> <config> [out.json]
+usage: tools/pmc_traffic.py <fetch_dir> <write_dir> <frames> <config> [out.json] [schedule]
 """
 import csv
 import glob
@@ -41,6 +41,7 @@ def load(d, counter):
 def main():
     fetch_dir, write_dir, frames, config = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
     out = sys.argv[5] if len(sys.argv) > 5 else None
+    schedule = sys.argv[6] if len(sys.argv) > 6 else "xa"
     fetch, fc = load(fetch_dir, "FETCH_SIZE")
     write, wc = load(write_dir, "WRITE_SIZE")
     steps_f = sum(v for k, v in fc.items() if k.startswith("welch_rows"))
@@ -55,11 +56,14 @@ def main():
                          "hbm_bytes_per_step_fetch_x2": int((2 * f_kib + w_kib) * 1024)}
         tot_raw += (f_kib + w_kib) * 1024
         tot_x2 += (2 * f_kib + w_kib) * 1024
-    res = {"frames": frames, "config": config, "steps_counted": [steps_f, steps_w],
+    res = {"frames": frames, "config": config, "schedule": schedule,
+           "steps_counted": [steps_f, steps_w],
            "hbm_bytes_per_step": int(tot_x2), "hbm_bytes_per_step_raw": int(tot_raw),
            "per_kernel": per_kernel,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
-                     "bench.py; FETCH doubled per the gfx950 calibration"}
+                     "bench.py; FETCH doubled per the gfx950 calibration (calibrated for 16-B-per-lane "
+                     "streaming reads; the XA stage loads are 8 B per lane, so the raw sum is "
+                     "kept as the lower bound)"}
     if out:
         json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
