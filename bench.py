@@ -42,7 +42,7 @@ CONFIGS = {
     "cfg4": dict(n_fft=4096, zoom=8, fs=2.4e6, n_avg=73, frames=4096, lo_step=150e3,
                  desc="8 independent IF centre frequencies (f_LO = 1 Hz + rank*150 kHz), one "
                       "stream per GPU"),
-    "cfg5": dict(n_fft=65536, zoom=8, fs=2.4e6, n_avg=16, frames=512,
+    "cfg5": dict(n_fft=65536, zoom=8, fs=2.4e6, n_avg=16, frames=2048,
                  desc="1M-sample frames, N_FFT=65536, four-step Welch; --in-dtype complex32 "
                       "for fp16 IQ storage"),
 }

@@ -545,7 +545,16 @@ int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
 constexpr int kEdge = 384;
 int64_t edge_window(int K) { return ((int64_t)1 << K) * (kEdge + 640); }
 
-constexpr int kXtMinFrames = 256;
+// Auto choice between XA (one wave per frame) and the blocked schedules, measured on
+// MI355X: XA needs >= 1024 waves to cover 2 waves x 1024 SIMDs well enough;
+// at 512 frames it still wins for ~300k-sample frames (2.21 vs 2.66 ms, cfg2) but loses for
+// 1M-sample frames (9.12 vs 8.38 ms, cfg5), whose blocked launch has 4x the blocks.
+constexpr int kXaMinFrames = 1024;
+constexpr int kXaMinFramesShort = 512;
+constexpr int64_t kXaShortFrame = (int64_t)1 << 19;
+bool auto_xa(int frames, int64_t L) {
+  return frames >= kXaMinFrames || (frames >= kXaMinFramesShort && L <= kXaShortFrame);
+}
 
 bool use_fused(const zfft_plan *p, int64_t L) {
   if (p->path == 1 || p->K < 2) return false;
@@ -689,7 +698,7 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  if (p->path == 4 || (p->path == 0 && frames >= kXtMinFrames))
+  if (p->path == 4 || (p->path == 0 && auto_xa(frames, L)))
     return run_xa(p, in, frames, n, out, st);
   if (p->path == 3) return run_xt(p, in, frames, n, out, st);
   if (use_fused(p, L)) return run_fused(p, in, L, frames, n, out, st);

@@ -112,7 +112,7 @@ class ZoomFFT:
 
     def set_path(self, path: int) -> None:
         """0 auto, 1 exact reference pass order, 2 fused interior + exact edges, 3 DF2T exact
-        tiles, 4 XA tiles (all-pole + FIR + half-rate all-pole; the auto choice for >= 256 frames)."""
+        tiles, 4 XA tiles (all-pole + FIR + half-rate all-pole; the auto choice for >= 1024 frames, or >= 512 frames of <= 2^19 samples)."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
 
     def set_welch(self, mode: int) -> None:

@@ -25,6 +25,9 @@ one 16-sample step back so a lane needs only its own and the previous lane's v. 
 backward pass of a tile starts from a provisional zero state at its top; its bottom exit
 state is exact and is the top state of the tile below (one-tile lag), whose top K kept
 outputs get the decaying correction Cm2full[d] . q (d = distance from the top).
+The HIP kernel applies the per-lane corrections as a second pass instead (it reruns each
+lane's sub-block from the exact entering state T . m_in, streaming the FIR), which is the
+same linear map; only the one-tile-lag correction of the held outputs is kept as modelled.
 
 Prints the fp64 model error (schedule exactness) and an fp32 emulation error vs scipy."""
 import numpy as np
