@@ -46,8 +46,9 @@ namespace xa {
 
 constexpr int kRow = kXaB + 2;          // LDS row stride (v2f): ds_read_b128 rows conflict-free
 constexpr int kHalfRows = 32;           // transposes go through LDS one half tile at a time
-constexpr int kBuf = kHalfRows * kRow + 16 + 64 + 32;  // + FIR carry (12 used) + frame-end v carry + LO chunk starts
 constexpr int kHeldRow = kXaK + 2;      // output-transpose rows (v2f): b128 writes conflict-free
+// + FIR carry (12 used) + frame-end v carry + LO chunk starts
+constexpr int kBuf = kHalfRows * kRow + 16 + 64 + 32;
 constexpr int kWaves = 2;               // waves (frames) per workgroup
 #ifndef XA_WAVES
 #define XA_WAVES 2                      // waves per SIMD the register budget is cut for
@@ -70,6 +71,12 @@ constexpr int kWaves = 2;               // waves (frames) per workgroup
 #endif
 #ifndef XA_LAG_EARLY
 #define XA_LAG_EARLY 1                  // lag rows loaded before the backward pass
+#endif
+#ifndef XA_BUFLOAD
+#define XA_BUFLOAD 1                    // next-tile loads through a range-checked buffer resource
+#endif
+#ifndef XA_ROWSCAN
+#define XA_ROWSCAN 1                    // modal scans on DPP rows + one cross-row step
 #endif
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -104,6 +111,23 @@ __device__ __forceinline__ v2f cvt_raw(typename Raw<DT>::T r) {  // as load_in_t
   if constexpr (DT == kInC64) return r;
   else if constexpr (DT == kInC32H) return v2f{(float)r.x, (float)r.y};
   else return v2f{((float)r.x - 127.5f) * (1.f / 127.5f), ((float)r.y - 127.5f) * (1.f / 127.5f)};
+}
+
+// one raw element through a buffer resource (out-of-range offsets read 0)
+template <class T>
+__device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  T v;
+  if constexpr (sizeof(T) == 8) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    __builtin_memcpy(&v, &u, 8);
+  } else if constexpr (sizeof(T) == 4) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    __builtin_memcpy(&v, &u, 4);
+  } else {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+    __builtin_memcpy(&v, &u, 2);
+  }
+  return v;
 }
 
 struct Md {
@@ -181,9 +205,29 @@ __device__ __forceinline__ void to_modal(CT tab, const v2f s[8], Md &m) {
 }
 
 // inclusive weighted scan over lanes: UP (lane i sums lanes j <= i) or down (j >= i),
-// m_i = sum_j lambda^(S |i-j|) m_j per mode
+// m_i = sum_j lambda^(S |i-j|) m_j per mode, every term within the mode's reach exact.
+// XA_ROWSCAN: modes 0, 1 run Kogge-Stone inside 16-lane rows on DPP row shifts, then add
+// the adjacent row's end lane (its within-row inclusive sum) weighted by the lane's own
+// distance to it (xw: c0 s0 c1 s1 for this lane-in-row): UP by DPP row_bcast:15, down by
+// one ds_bpermute round; modes 2, 3 need one whole-wave DPP shift.  Otherwise the older
+// whole-wave form (DPP first level, ds_bpermute chains after).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ v2f dpp0(v2f src) {  // lanes without a source (or row) get 0
+  return v2f{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(src.x), CTRL, ROWMASK, 0xF, false)),
+             __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(src.y), CTRL, ROWMASK, 0xF, false))};
+}
+constexpr int kRowShr = 0x110, kRowShl = 0x100, kRowBcast15 = 0x142;
+template <bool UP>
+__device__ __forceinline__ v2f row_shift(v2f src, int d) {  // by 2^d lanes inside 16-lane rows
+  switch (d) {
+    case 0: return dpp0<(UP ? kRowShr : kRowShl) + 1, 0xF>(src);
+    case 1: return dpp0<(UP ? kRowShr : kRowShl) + 2, 0xF>(src);
+    case 2: return dpp0<(UP ? kRowShr : kRowShl) + 4, 0xF>(src);
+    default: return dpp0<(UP ? kRowShr : kRowShl) + 8, 0xF>(src);
+  }
+}
 template <int PASS, bool UP>
-__device__ __forceinline__ void modal_scan(Md &m, CT tab, int lane) {
+__device__ __forceinline__ void modal_scan(Md &m, CT tab, int lane, v4f xw) {
   asm volatile("" : "+v"(lane));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -192,7 +236,10 @@ __device__ __forceinline__ void modal_scan(Md &m, CT tab, int lane) {
       CT t = fresh(tab);
       float c = pass_of<PASS>(t).scan[d][j][0], sn = pass_of<PASS>(t).scan[d][j][1];
       v2f pa, pb;
-      if (d == 0) {
+      if (XA_ROWSCAN && j < kXaRowModes) {
+        pa = row_shift<UP>(m.r[2 * j], d);
+        pb = row_shift<UP>(m.r[2 * j + 1], d);
+      } else if (d == 0) {
         constexpr int ctrl = UP ? kShr1 : kShl1;
         pa = wave_shift<ctrl>(splat(0.f), m.r[2 * j]);
         pb = wave_shift<ctrl>(splat(0.f), m.r[2 * j + 1]);
@@ -208,6 +255,28 @@ __device__ __forceinline__ void modal_scan(Md &m, CT tab, int lane) {
       rot(pa, pb, c, sn);
       m.r[2 * j] += pa;
       m.r[2 * j + 1] += pb;
+    }
+  }
+  if (XA_ROWSCAN) {
+    v2f pa[kXaRowModes], pb[kXaRowModes];
+#pragma unroll
+    for (int j = 0; j < kXaRowModes; ++j) {
+      if (UP) {  // rows 1..3 <- lane 15 of the row below
+        pa[j] = dpp0<kRowBcast15, 0xE>(m.r[2 * j]);
+        pb[j] = dpp0<kRowBcast15, 0xE>(m.r[2 * j + 1]);
+      } else {   // rows 0..2 <- lane 0 of the row above
+        const int src = ((lane | 15) + 1) & 63;
+        pa[j] = shfl2(m.r[2 * j], src);
+        pb[j] = shfl2(m.r[2 * j + 1], src);
+      }
+    }
+    const bool take = UP || lane < 48;
+#pragma unroll
+    for (int j = 0; j < kXaRowModes; ++j) {
+      const float c = take ? (j == 0 ? xw.x : xw.z) : 0.f, sn = take ? (j == 0 ? xw.y : xw.w) : 0.f;
+      rot(pa[j], pb[j], c, sn);
+      m.r[2 * j] += pa[j];
+      m.r[2 * j + 1] += pb[j];
     }
   }
 }
@@ -267,8 +336,10 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
 #if XA_LAG_LDS
   __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];
   for (int i = threadIdx.x; i < kXaLag * 2; i += 64 * kWaves) lag_l[i] = ((const v4f *)tab_g->lag)[i];
-  __syncthreads();
 #endif
+  __shared__ v4f xw_l[2][16];  // cross-row scan weights (XaPass::xr), forward / backward
+  if (threadIdx.x < 32) xw_l[threadIdx.x >> 4][threadIdx.x & 15] = ((const v4f *)((threadIdx.x >> 4) ? tab_g->b.xr : tab_g->f.xr))[threadIdx.x & 15];
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR
   const int f = blockIdx.x * kWaves + wv;
@@ -310,15 +381,15 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
   }
   __builtin_amdgcn_wave_barrier();
 
+  constexpr int kChunks = kXaT / 2 / 64;
+  constexpr int kLagChunks = kXaLag / 64;
+  auto m_of = [&](int tile, int idx) { return tile * (kXaT / 2) - (kPad + 15) / 2 + idx; };
   // Tile outputs -> frame row through LDS transposes (64 consecutive outputs per store
   // instruction), one half tile at a time.  Chunks below the top kXaLag outputs are final
   // at once; the top chunks wait in registers for the next tile's exact top state q.
-  constexpr int kChunks = kXaT / 2 / 64;
-  constexpr int kLagChunks = kXaLag / 64;
   v2f held[kLagChunks];
 #pragma unroll
   for (int c = 0; c < kLagChunks; ++c) held[c] = splat(0.f);
-  auto m_of = [&](int tile, int idx) { return tile * (kXaT / 2) - (kPad + 15) / 2 + idx; };
   auto flush_tile = [&](int tile, const v2f *h, int ln) {
     const int m0 = m_of(tile, ln);
     v2f *__restrict__ od = o + m0;
@@ -385,6 +456,23 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
   const RawT *pnext = src;
   bool next_fast = false;
   int next_i0 = 0;  // first input index of the next tile
+#if XA_BUFLOAD
+  // next-tile loads through a range-checked buffer resource over the frame, issued for
+  // every tile (out-of-range lanes read 0; an edge tile never reads them): pf is then dead
+  // between its use at the tile start and its reload, where a conditional reload would
+  // keep all of pf live across the whole tile
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)src, (short)0, (int)(in.len * (int64_t)sizeof(RawT)), 0x00020000);
+  uint32_t next_off = 0;  // byte offset of this lane's element of the next tile's chunk 0
+  auto issue_group = [&](int g) {
+    if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + 64 * (lane & 31)];
+    if (XA_SPREAD && 4 * g < XA_PF) {
+#pragma unroll
+      for (int q = 4 * g; q < 4 * g + 4 && q < XA_PF; ++q)
+        pf[q < kPfc ? q : 0] = buf_load<RawT>(rsrc, next_off + (uint32_t)((FLIP ? -64 : 64) * q * (int)sizeof(RawT)));
+    }
+  };
+#else
   auto issue_group = [&](int g) {
     if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + 64 * (lane & 31)];
     if (XA_SPREAD && next_fast && 4 * g < XA_PF) {
@@ -392,6 +480,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
       for (int q = 4 * g; q < 4 * g + 4 && q < XA_PF; ++q) pf[q < kPfc ? q : 0] = pnext[FLIP ? -64 * q : 64 * q];
     }
   };
+#endif
 
 #if XA_STAMPS
   unsigned long long st_acc[kStampSegs] = {}, t_prev;
@@ -475,6 +564,9 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     {
       const int i0 = base + kXaT - kPad + ln;
       pnext = src + (FLIP ? in.len - 1 - i0 : i0);
+#if XA_BUFLOAD
+      next_off = (uint32_t)((FLIP ? in.len - 1 - i0 : (int64_t)i0) * (int64_t)sizeof(RawT));
+#endif
     }
     issue_group(0);
     XA_STAMP(0);
@@ -499,7 +591,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         XA_STAMP(1);
         issue_group(1);
         fold_entering<0>(m, m_in, tab, ln == 0);
-        modal_scan<0, true>(m, tab, ln);
+        modal_scan<0, true>(m, tab, ln, xw_l[0][ln & 15]);
 #pragma unroll
         for (int r = 0; r < 8; ++r) me.r[r] = wave_shift<kShr1>(m_in.r[r], m.r[r]);
 #pragma unroll
@@ -680,7 +772,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
           for (int r = 0; r < 8; ++r) qtop.r[r] = last ? tb->b.ss[r] * h_ss : splat(0.f);
         }
         if (last) fold_entering<1>(m, qtop, tab, ln == 63);
-        modal_scan<1, false>(m, tab, ln);
+        modal_scan<1, false>(m, tab, ln, xw_l[1][ln & 15]);
 #pragma unroll
         for (int r = 0; r < 8; ++r) qe.r[r] = wave_shift<kShl1>(qtop.r[r], m.r[r]);
 #pragma unroll

@@ -105,8 +105,11 @@ constexpr int kXaT = 64 * kXaB;      // tile (forward samples)
 constexpr int kXaK = kXaB / 2;       // kept outputs per lane and tile
 constexpr int kXaLag = 192;          // held-tile outputs corrected by the one-tile lag
 // scan levels per mode (modes follow the cascade order, slowest pole first): mode j needs
-// |lambda_j|^(S 2^levels) < 1e-9; checked when the tables are built
+// |lambda_j|^(S 2^levels) < 1e-9; checked when the tables are built.  Modes 0, 1 scan
+// inside 16-lane rows (DPP row shifts, <= 4 levels) and then add the adjacent row's end
+// lane; modes 2, 3 take one whole-wave shift (1 level).
 constexpr int kXaLevels[4] = {4, 2, 1, 1};
+constexpr int kXaRowModes = 2;
 struct XaPass {                      // one all-pole cascade, DF-I state (y[t-1], y[t-2]) per section
   float a1[4], a2[4];                // y = x - a1 y[t-1] - a2 y[t-2], cascade order
   float ti[8][8];                    // T^-1: state -> real modal (block lower triangular)
@@ -114,6 +117,9 @@ struct XaPass {                      // one all-pole cascade, DF-I state (y[t-1]
   float ss[8];                       // modal steady state per unit constant input
   float pS[4][2];                    // lambda_j^S (one lane sub-block of S steps)
   float scan[4][4][2];               // lambda_j^(S 2^d), scan level d
+  // modes 0, 1 cross the 16-lane DPP rows once: weight lambda_j^(S dist) of the adjacent
+  // row's end lane for lane-in-row i (dist = i + 1 forward, 16 - i backward): c0 s0 c1 s1
+  alignas(16) float xr[16][4];
 };
 struct XaTab {
   XaPass f, b;                       // forward (full rate, S = kXaB), backward (S = kXaK)
@@ -123,7 +129,7 @@ struct XaTab {
   float mp_sum;                      // h per unit constant f (backward steady input)
   float vss;                         // forward cascade output per unit constant input
   float pad_[2];
-  float lag[kXaLag][8];              // backward C A2^d T: held output d steps below the top
+  alignas(16) float lag[kXaLag][8];  // backward C A2^d T: held output d steps below the top
 };
 
 hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix,

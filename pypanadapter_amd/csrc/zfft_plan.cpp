@@ -235,7 +235,7 @@ void modal_basis(const Mat8 &A, const cd lam[4], Mat8 &T) {
 
 // One pass: fills P, the output table cm (steps rows) and, when lag != nullptr, the
 // far-field rows C A^d T for d < n_lag.
-bool xa_pass_tables(const ApD &c, int steps, XaPass &P, float (*lag)[8], int n_lag) {
+bool xa_pass_tables(const ApD &c, int steps, bool up, XaPass &P, float (*lag)[8], int n_lag) {
   Mat8 A(64);
   double C[8];
   for (int q = 0; q < 8; ++q) {
@@ -278,6 +278,16 @@ bool xa_pass_tables(const ApD &c, int steps, XaPass &P, float (*lag)[8], int n_l
       P.scan[d][j][1] = (float)u.imag();
     }
   }
+  for (int i = 0; i < 16; ++i)
+    for (int j = 0; j < 4; ++j) P.xr[i][j] = 0.f;
+  for (int j = 0; j < kXaRowModes; ++j) {
+    if (kXaLevels[j] > 4) return false;  // row shifts reach at most 8 lanes
+    for (int i = 0; i < 16; ++i) {
+      const cd u = std::pow(lam[j], steps * (up ? i + 1 : 16 - i));
+      P.xr[i][2 * j] = (float)u.real();
+      P.xr[i][2 * j + 1] = (float)u.imag();
+    }
+  }
   Mat8 AtT = T;  // A^t T
   for (int t = 0; lag && t < n_lag; ++t) {
     for (int q = 0; q < 8; ++q) {
@@ -300,7 +310,8 @@ bool xa_build_tables(XaTab &X) {
     bw.a1[k] = 2.0 * a2 - a1 * a1;  // D(z) D(-z) = D2(z^2)
     bw.a2[k] = a2 * a2;
   }
-  if (!xa_pass_tables(fw, kXaB, X.f, nullptr, 0) || !xa_pass_tables(bw, kXaK, X.b, X.lag, kXaLag))
+  if (!xa_pass_tables(fw, kXaB, true, X.f, nullptr, 0) ||
+      !xa_pass_tables(bw, kXaK, false, X.b, X.lag, kXaLag))
     return false;
   // N = b0 (1 + z^-1)^8 (sections 1..3 are exactly [1, 2, 1], section 0 is b0 [1, 2, 1])
   double n9[9], dneg[9] = {1.0}, mp[17] = {0}, m25[25] = {0};

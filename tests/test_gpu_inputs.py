@@ -48,7 +48,7 @@ def test_input_format_rows_vs_oracle(oracle_lib, fmt, flip, N, z, L, F):
     arr, vals = _encode(x, fmt)
     ref_in = vals[:, ::-1] if flip else vals
     refs = [oracle_lib.psd_row(ref_in[f], 2.4e6, N, z, W) for f in range(F)]
-    for path in ([0, 1, 3] if z > 1 else [0]):
+    for path in ([0, 1, 3, 4] if z > 1 else [0]):
         with ZoomFFT(N, z, 2.4e6, n_win=W, in_dtype=fmt, flip=flip) as plan:
             plan.set_path(path)
             rows = plan.rows(arr)

@@ -11,8 +11,8 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pypanadapter_amd import ZoomFFT, _lib  # noqa: E402
 
-SEGS = ["load+transpose", "fwd AP+modal", "fwd scan", "fwd corr", "v->LDS+FIR", "tail+halo",
-        "bwd AP+modal", "bwd scan+corr", "finish_held", "flush"]
+SEGS = ["load+transpose", "fwd pass 1+modal", "fwd scan", "fwd pass 2+FIR+P", "frame-end v",
+        "frame-end f/h", "bwd pass 1+modal", "bwd scan+pass 2", "finish_held", "flush"]
 
 
 def main():
