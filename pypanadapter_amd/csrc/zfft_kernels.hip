@@ -761,6 +761,162 @@ __global__ __launch_bounds__(MAXT) void welch_rows2_kernel(const v2f *__restrict
   }
 }
 
+// ------------------------------------------------------------------ Welch row, N = 4096
+// In-place radix-16 decimation in frequency, one workgroup (256 threads, 16 values each)
+// per frame.  With n = 256 n2 + 16 n1 + n0 and k = k0 + 16 k1 + 256 k2:
+//   stage 1  thread t = 16 n1 + n0: DFT16 over n2 (its own loads), x W_4096^(t k0)
+//   stage 2  thread (k0, n0) = (t / 16, t % 16): DFT16 over n1, x W_256^(n0 k1)
+//   stage 3  thread (k0, k1) = (t / 16, t % 16): DFT16 over n0 -> X[k0 + 16 k1 + 256 k2]
+// Every stage reads and writes back the same LDS slots (position 256 k0 + 16 n1|k1 + n0),
+// so a stage needs no barrier between its reads and its writes: three barriers per segment
+// (after the stage-1 and stage-2 stores, and before the next segment's stage-1 stores)
+// against the Stockham kernel's six.  The constant-detrend mean of segment s+1 is reduced
+// from its prefetched registers during segment s (partial sums posted before segment s's
+// second barrier, by segment parity), and the twiddles are rebuilt per segment from four
+// powers per stage held in registers (w, w^2, w^4, w^8; at most three products deep).
+// PRUNE (W <= 512): only bins k2 in {0, 15} reach the fftshift crop, so stage 3 forms just
+// those two outputs.
+#ifndef WELCH_DIF_WAVES
+#define WELCH_DIF_WAVES 3  // waves per SIMD the registers are cut for (PRUNE; the full form: 2)
+#endif
+__host__ __device__ constexpr int dif_slot(int i) { return i + (i >> 4); }  // conflict-free strides 1, 16
+
+// w[r] = b^r, r = 1..15, from bp = {b, b^2, b^4, b^8}
+__device__ __forceinline__ void tw_powers(const v2f *bp, v2f *w) {
+  w[1] = bp[0];
+  w[2] = bp[1];
+  w[4] = bp[2];
+  w[8] = bp[3];
+  w[3] = cmul(w[1], w[2]);
+  w[5] = cmul(w[1], w[4]);
+  w[6] = cmul(w[2], w[4]);
+  w[7] = cmul(w[3], w[4]);
+  w[9] = cmul(w[1], w[8]);
+  w[10] = cmul(w[2], w[8]);
+  w[11] = cmul(w[3], w[8]);
+  w[12] = cmul(w[4], w[8]);
+  w[13] = cmul(w[5], w[8]);
+  w[14] = cmul(w[6], w[8]);
+  w[15] = cmul(w[7], w[8]);
+}
+
+template <bool PRUNE>
+__global__ __launch_bounds__(256, PRUNE ? WELCH_DIF_WAVES : 2) void welch_dif4096_kernel(const v2f *__restrict__ x, int64_t len,
+                                                               const float *__restrict__ win,
+                                                               const v2f *__restrict__ tw, WelchGeom g,
+                                                               float *__restrict__ rows, int frames) {
+  constexpr int N = 4096, T = 256;
+  __shared__ v2f img[dif_slot(N - 1) + 1];
+  __shared__ v2f red[2][4];  // wave partial sums of the segment mean, by segment parity
+  const int t = threadIdx.x;
+  int f = blockIdx.x;
+  if ((frames & 7) == 0 && frames >= 64)  // spread consecutive frames over the 8 XCDs evenly
+    f = (blockIdx.x & 7) * (frames >> 3) + (blockIdx.x >> 3);
+  const v2f *__restrict__ xf = x + (int64_t)f * len;
+  // twiddle bases: stage 1 W_4096^(t m), stage 2 W_4096^(16 (t % 16) m), m = 1, 2, 4, 8
+  v2f b1[4], b2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    b1[i] = tw[(t << i) & (N - 1)];
+    b2[i] = tw[((16 * (t & 15)) << i) & (N - 1)];
+  }
+
+  auto load_seg = [&](v2f *dst, int s) {
+    const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[r] = seg[t + T * r];
+  };
+  auto post_sum = [&](const v2f *v, int slot) {
+    v2f sum = splat(0.f);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sum += v[r];
+    sum = wave_sum(sum);
+    if ((t & 63) == 0) red[slot][t >> 6] = sum;
+  };
+  v2f pf[16];
+  load_seg(pf, 0);
+  post_sum(pf, 0);
+  __syncthreads();
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+
+  for (int s = 0; s < g.nseg; ++s) {
+    // opaque per-segment copies: the twiddle powers and LDS addresses are rebuilt in the
+    // loop rather than hoisted out of it (60 + 48 registers held across the loop)
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      asm volatile("" : "+v"(b1[i]));
+      asm volatile("" : "+v"(b2[i]));
+    }
+    v2f v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = pf[r];
+    const bool more = s + 1 < g.nseg;
+    if (more) load_seg(pf, s + 1);  // in flight during this segment's transform
+    {
+      const v2f mean = (red[s & 1][0] + red[s & 1][1] + red[s & 1][2] + red[s & 1][3]) * (1.f / (float)N);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = (v[r] - mean) * win[t + T * r];
+    }
+    // stage 1: DFT over n2, twiddle W_4096^(t k0), store at 256 k0 + t
+    dft<16>(v);
+    {
+      v2f w[16];
+      tw_powers(b1, w);
+#pragma unroll
+      for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], w[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) img[dif_slot(T * k + t)] = v[k];
+    __syncthreads();
+    // stage 2: thread (k0, n0); DFT over n1, twiddle W_256^(n0 k1), back to the same slots
+    {
+      const int base = 256 * (t >> 4) + (t & 15);
+#pragma unroll
+      for (int n = 0; n < 16; ++n) v[n] = img[dif_slot(base + 16 * n)];
+      dft<16>(v);
+      v2f w[16];
+      tw_powers(b2, w);
+#pragma unroll
+      for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], w[k]);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) img[dif_slot(base + 16 * k)] = v[k];
+    }
+    if (more) post_sum(pf, (s + 1) & 1);  // the next segment's mean, read after two barriers
+    __syncthreads();
+    // stage 3: thread (k0, k1); DFT over n0 -> bins k0 + 16 k1 + 256 k2
+#pragma unroll
+    for (int n = 0; n < 16; ++n) v[n] = img[dif_slot(16 * t + n)];
+    if constexpr (PRUNE) {  // k2 = 0 and k2 = 15 only: X_15 = sum_n v_n W16^(15 n) = sum_n v_n conj(W16^n)
+      v2f a0 = splat(0.f), a15 = splat(0.f);
+#pragma unroll
+      for (int n = 0; n < 16; ++n) {
+        a0 += v[n];
+        const v2f wc = w16(16 - n);  // W16^(-n) = W16^(15 n) (mod 16)
+        a15 += cmul(v[n], wc);
+      }
+      acc[0] = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, acc[0]));
+      acc[15] = fmaf(a15.x, a15.x, fmaf(a15.y, a15.y, acc[15]));
+    } else {
+      dft<16>(v);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[k] = fmaf(v[k].x, v[k].x, fmaf(v[k].y, v[k].y, acc[k]));
+    }
+    __syncthreads();  // stage-3 reads done before the next segment's stage-1 stores
+  }
+  float *__restrict__ row = rows + (int64_t)f * g.n_win;
+#pragma unroll
+  for (int k2 = 0; k2 < 16; ++k2) {
+    if (PRUNE && k2 != 0 && k2 != 15) continue;
+    const int k = (t >> 4) + 16 * (t & 15) + 256 * k2;
+    const int j = (k + (g.n_win >> 1)) & (N - 1);  // fftshift + crop: row[j] = P[(j - W/2) mod N]
+    if (j < g.n_win) row[j] = 20.f * log10f(acc[k2] * g.scale);
+  }
+}
+
 // ------------------------------------------------------------------ Welch row, four-step
 // N = N1 * N2 (N2 = 256) for segments too long for one workgroup's LDS (N = 32768 is in
 // the reference UI's range S:1397, N = 65536 is BASELINE cfg5).  With n = n1 + N1 n2 and
@@ -1042,9 +1198,21 @@ static hipError_t welch2_launch_t(const float2 *x, int64_t len, const float *win
 #ifndef WELCH_V2
 #define WELCH_V2 0  // v2 (mean one segment ahead, 2 barriers) measured slower on MI355X: 1.36 vs 1.19 ms at cfg2
 #endif
+#ifndef WELCH_DIF
+#define WELCH_DIF 1
+#endif
 template <int R0>
 static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
                                const WelchGeom &g, float *rows, int frames, hipStream_t st) {
+  if (WELCH_DIF && g.n_fft == 4096 && g.nperseg == 4096) {
+    if (g.n_win <= 512)
+      hipLaunchKernelGGL(welch_dif4096_kernel<true>, dim3(frames), dim3(256), 0, st, (const v2f *)x, len, win,
+                         (const v2f *)tw, g, rows, frames);
+    else
+      hipLaunchKernelGGL(welch_dif4096_kernel<false>, dim3(frames), dim3(256), 0, st, (const v2f *)x, len, win,
+                         (const v2f *)tw, g, rows, frames);
+    return hipGetLastError();
+  }
   if (WELCH_V2 && g.n_fft <= 4096) return welch2_launch_t<R0, 256>(x, len, win, tw, g, rows, frames, st);
   if (WELCH_V2 && g.n_fft <= 8192) return welch2_launch_t<R0, 512>(x, len, win, tw, g, rows, frames, st);
   // threads = N/16 (>= 64): N <= 4096 -> <= 256 threads, room for the prefetch registers
