@@ -213,8 +213,12 @@ __device__ __forceinline__ void to_modal(CT tab, const v2f s[8], Md &m) {
 // whole-wave form (DPP first level, ds_bpermute chains after).
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ v2f dpp0(v2f src) {  // lanes without a source (or row) get 0
-  return v2f{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(src.x), CTRL, ROWMASK, 0xF, false)),
-             __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(src.y), CTRL, ROWMASK, 0xF, false))};
+  if constexpr (ROWMASK == 0xF)  // bound_ctrl: a lane without a source reads 0, no old value
+    return v2f{__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(src.x), CTRL, 0xF, 0xF, true)),
+               __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(src.y), CTRL, 0xF, 0xF, true))};
+  else
+    return v2f{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(src.x), CTRL, ROWMASK, 0xF, false)),
+               __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(src.y), CTRL, ROWMASK, 0xF, false))};
 }
 constexpr int kRowShr = 0x110, kRowShl = 0x100, kRowBcast15 = 0x142;
 template <bool UP>
@@ -241,8 +245,8 @@ __device__ __forceinline__ void modal_scan(Md &m, CT tab, int lane, v4f xw) {
         pb = row_shift<UP>(m.r[2 * j + 1], d);
       } else if (d == 0) {
         constexpr int ctrl = UP ? kShr1 : kShl1;
-        pa = wave_shift<ctrl>(splat(0.f), m.r[2 * j]);
-        pb = wave_shift<ctrl>(splat(0.f), m.r[2 * j + 1]);
+        pa = dpp0<ctrl, 0xF>(m.r[2 * j]);
+        pb = dpp0<ctrl, 0xF>(m.r[2 * j + 1]);
       } else {
         const int sh = 1 << d;
         const bool take = UP ? lane >= sh : lane + sh <= 63;

@@ -776,28 +776,37 @@ __global__ __launch_bounds__(MAXT) void welch_rows2_kernel(const v2f *__restrict
 // powers per stage held in registers (w, w^2, w^4, w^8; at most three products deep).
 // PRUNE (W <= 512): only bins k2 in {0, 15} reach the fftshift crop, so stage 3 forms just
 // those two outputs.
+#ifndef WELCH_DIF_PF
+#define WELCH_DIF_PF 16  // values per thread prefetched a segment ahead
+#endif
+#ifndef WELCH_DIF_B2
+#define WELCH_DIF_B2 1  // stage-2 twiddle bases held in registers (0: re-read per segment)
+#endif
 #ifndef WELCH_DIF_WAVES
 #define WELCH_DIF_WAVES 3  // waves per SIMD the registers are cut for (PRUNE; the full form: 2)
 #endif
 __host__ __device__ constexpr int dif_slot(int i) { return i + (i >> 4); }  // conflict-free strides 1, 16
 
-// w[r] = b^r, r = 1..15, from bp = {b, b^2, b^4, b^8}
-__device__ __forceinline__ void tw_powers(const v2f *bp, v2f *w) {
-  w[1] = bp[0];
-  w[2] = bp[1];
-  w[4] = bp[2];
-  w[8] = bp[3];
-  w[3] = cmul(w[1], w[2]);
-  w[5] = cmul(w[1], w[4]);
-  w[6] = cmul(w[2], w[4]);
-  w[7] = cmul(w[3], w[4]);
-  w[9] = cmul(w[1], w[8]);
-  w[10] = cmul(w[2], w[8]);
-  w[11] = cmul(w[3], w[8]);
-  w[12] = cmul(w[4], w[8]);
-  w[13] = cmul(w[5], w[8]);
-  w[14] = cmul(w[6], w[8]);
-  w[15] = cmul(w[7], w[8]);
+// v[r] *= b^r, r = 1..15, from bp = {b, b^2, b^4, b^8}: each power applied as soon as it
+// is formed (at most eight of them live)
+__device__ __forceinline__ void apply_powers(v2f *v, const v2f *bp) {
+  v[1] = cmul(v[1], bp[0]);
+  v[2] = cmul(v[2], bp[1]);
+  v[4] = cmul(v[4], bp[2]);
+  v[8] = cmul(v[8], bp[3]);
+  const v2f w3 = cmul(bp[0], bp[1]), w5 = cmul(bp[0], bp[2]), w6 = cmul(bp[1], bp[2]);
+  const v2f w7 = cmul(w3, bp[2]);
+  v[3] = cmul(v[3], w3);
+  v[5] = cmul(v[5], w5);
+  v[6] = cmul(v[6], w6);
+  v[7] = cmul(v[7], w7);
+  v[9] = cmul(v[9], cmul(bp[0], bp[3]));
+  v[10] = cmul(v[10], cmul(bp[1], bp[3]));
+  v[11] = cmul(v[11], cmul(w3, bp[3]));
+  v[12] = cmul(v[12], cmul(bp[2], bp[3]));
+  v[13] = cmul(v[13], cmul(w5, bp[3]));
+  v[14] = cmul(v[14], cmul(w6, bp[3]));
+  v[15] = cmul(v[15], cmul(w7, bp[3]));
 }
 
 template <bool PRUNE>
@@ -813,29 +822,34 @@ __global__ __launch_bounds__(256, PRUNE ? WELCH_DIF_WAVES : 2) void welch_dif409
   if ((frames & 7) == 0 && frames >= 64)  // spread consecutive frames over the 8 XCDs evenly
     f = (blockIdx.x & 7) * (frames >> 3) + (blockIdx.x >> 3);
   const v2f *__restrict__ xf = x + (int64_t)f * len;
-  // twiddle bases: stage 1 W_4096^(t m), stage 2 W_4096^(16 (t % 16) m), m = 1, 2, 4, 8
+  // twiddle bases: stage 1 W_4096^(t m) held, stage 2 W_4096^(16 (t % 16) m) re-read per
+  // segment (L1 hits; WELCH_DIF_B2 holds them too), m = 1, 2, 4, 8
   v2f b1[4], b2[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     b1[i] = tw[(t << i) & (N - 1)];
-    b2[i] = tw[((16 * (t & 15)) << i) & (N - 1)];
+    if (WELCH_DIF_B2) b2[i] = tw[((16 * (t & 15)) << i) & (N - 1)];
   }
 
   auto load_seg = [&](v2f *dst, int s) {
     const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dst[r] = seg[t + T * r];
+    for (int r = 0; r < WELCH_DIF_PF; ++r) dst[r] = seg[t + T * r];
   };
-  auto post_sum = [&](const v2f *v, int slot) {
+  // partial sums of segment s: the prefetched values plus a separate pass over the rest
+  auto post_sum = [&](const v2f *v, int slot, int s) {
     v2f sum = splat(0.f);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sum += v[r];
+    for (int r = 0; r < WELCH_DIF_PF; ++r) sum += v[r];
+    const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
+#pragma unroll
+    for (int r = WELCH_DIF_PF; r < 16; ++r) sum += seg[t + T * r];
     sum = wave_sum(sum);
     if ((t & 63) == 0) red[slot][t >> 6] = sum;
   };
-  v2f pf[16];
+  v2f pf[WELCH_DIF_PF > 0 ? WELCH_DIF_PF : 1];
   load_seg(pf, 0);
-  post_sum(pf, 0);
+  post_sum(pf, 0, 0);
   __syncthreads();
   float acc[16];
 #pragma unroll
@@ -849,11 +863,15 @@ __global__ __launch_bounds__(256, PRUNE ? WELCH_DIF_WAVES : 2) void welch_dif409
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       asm volatile("" : "+v"(b1[i]));
-      asm volatile("" : "+v"(b2[i]));
+      if (WELCH_DIF_B2) asm volatile("" : "+v"(b2[i]));
+      else b2[i] = tw[((16 * (t & 15)) << i) & (N - 1)];
     }
     v2f v[16];
+    {  // values [0, WELCH_DIF_PF) were prefetched a segment ahead, the rest load now
+      const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = pf[r];
+      for (int r = 0; r < 16; ++r) v[r] = r < WELCH_DIF_PF ? pf[r] : seg[t + T * r];
+    }
     const bool more = s + 1 < g.nseg;
     if (more) load_seg(pf, s + 1);  // in flight during this segment's transform
     {
@@ -863,12 +881,7 @@ __global__ __launch_bounds__(256, PRUNE ? WELCH_DIF_WAVES : 2) void welch_dif409
     }
     // stage 1: DFT over n2, twiddle W_4096^(t k0), store at 256 k0 + t
     dft<16>(v);
-    {
-      v2f w[16];
-      tw_powers(b1, w);
-#pragma unroll
-      for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], w[k]);
-    }
+    apply_powers(v, b1);
 #pragma unroll
     for (int k = 0; k < 16; ++k) img[dif_slot(T * k + t)] = v[k];
     __syncthreads();
@@ -878,14 +891,11 @@ __global__ __launch_bounds__(256, PRUNE ? WELCH_DIF_WAVES : 2) void welch_dif409
 #pragma unroll
       for (int n = 0; n < 16; ++n) v[n] = img[dif_slot(base + 16 * n)];
       dft<16>(v);
-      v2f w[16];
-      tw_powers(b2, w);
-#pragma unroll
-      for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], w[k]);
+      apply_powers(v, b2);
 #pragma unroll
       for (int k = 0; k < 16; ++k) img[dif_slot(base + 16 * k)] = v[k];
     }
-    if (more) post_sum(pf, (s + 1) & 1);  // the next segment's mean, read after two barriers
+    if (more) post_sum(pf, (s + 1) & 1, s + 1);  // the next segment's mean, read after two barriers
     __syncthreads();
     // stage 3: thread (k0, k1); DFT over n0 -> bins k0 + 16 k1 + 256 k2
 #pragma unroll
