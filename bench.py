@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--warm", type=int, default=0)
     ap.add_argument("--path", type=int, default=0,
                     help="0 auto, 1 exact order, 2 fused interior, 3 DF2T exact tiles, 4 XA tiles")
+    ap.add_argument("--welch", type=int, default=0,
+                    help="Welch kernel: 0 auto, 1 one workgroup per frame, 2 four-step (A/B runs)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -165,6 +167,8 @@ def main():
         plan.tune(args.block, args.warm)
     if args.path:
         plan.set_path(args.path)
+    if args.welch:
+        plan.set_welch(args.welch)
     stream = torch.cuda.Stream(dev)  # a real stream: the null stream's handle (0) would be
     torch.cuda.set_stream(stream)    # read by the C-ABI as "the plan's own stream"
     sp = stream.cuda_stream
@@ -244,7 +248,7 @@ def main():
             tj = json.load(open(tpath))
             if (tj.get("frames") == F and tj.get("in_dtype", "complex64") == args.in_dtype
                     and tj.get("schedule") == "xa"  # measured on the current auto schedule
-                    and not args.path and not args.block and not args.warm):
+                    and not args.path and not args.welch and not args.block and not args.warm):
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None

@@ -761,31 +761,56 @@ __global__ __launch_bounds__(MAXT) void welch_rows2_kernel(const v2f *__restrict
   }
 }
 
-// ------------------------------------------------------------------ Welch row, N = 4096
-// In-place radix-16 decimation in frequency, one workgroup (256 threads, 16 values each)
-// per frame.  With n = 256 n2 + 16 n1 + n0 and k = k0 + 16 k1 + 256 k2:
-//   stage 1  thread t = 16 n1 + n0: DFT16 over n2 (its own loads), x W_4096^(t k0)
-//   stage 2  thread (k0, n0) = (t / 16, t % 16): DFT16 over n1, x W_256^(n0 k1)
-//   stage 3  thread (k0, k1) = (t / 16, t % 16): DFT16 over n0 -> X[k0 + 16 k1 + 256 k2]
-// Every stage reads and writes back the same LDS slots (position 256 k0 + 16 n1|k1 + n0),
-// so a stage needs no barrier between its reads and its writes: three barriers per segment
-// (after the stage-1 and stage-2 stores, and before the next segment's stage-1 stores)
-// against the Stockham kernel's six.  The constant-detrend mean of segment s+1 is reduced
-// from its prefetched registers during segment s (partial sums posted before segment s's
-// second barrier, by segment parity), and the twiddles are rebuilt per segment from four
-// powers per stage held in registers (w, w^2, w^4, w^8; at most three products deep).
-// PRUNE (W <= 512): only bins k2 in {0, 15} reach the fftshift crop, so stage 3 forms just
-// those two outputs.
+// ------------------------------------------------------------------ Welch row, in-place DIF
+// N = 16^P R0 (R0 in {1, 2, 4, 8}), 1024 <= N <= 16384: T = N/16 threads per frame, 16
+// values each, FPB = 256/T frames per workgroup when T < 256 (a frame is then one wave).
+// Gentleman-Sande in-place decimation in frequency: radix-16 stage s (span M = N/16^(s-1),
+// stride M/16) gives thread t the block b = t / (M/16) and offset j = t % (M/16); it forms
+// the DFT16 of the slots b M + j + (M/16) m and writes X_k W_M^(j k) back to the slots it
+// read (k in place of m).  The last stage (radix RL = R0, or 16 when R0 = 1) takes the
+// thread's 16 consecutive slots as 16/RL blocks of RL.  Slot Q = sum_s d_s N/16^s (+ d_(P+1))
+// then holds bin k = sum_s d_s 16^(s-1) (+ 16^P d_(P+1)): the digits reversed.
+// Stage 1 is the thread's own loads x[t + T m] (coalesced), so the window and the
+// constant-detrend mean apply in registers first.  A stage writes back only the slots it
+// read, so it needs no barrier between its reads and writes: one barrier after each
+// stage's stores and one before the next segment's first stores -- 3 per segment at
+// N = 4096 against the Stockham kernel's 6, and only wave barriers when a frame is one wave.
+// The mean of segment s+1 is reduced from its prefetched registers during segment s
+// (posted before segment s's last barrier, by segment parity); the twiddles are rebuilt
+// per segment from four powers per stage (w, w^2, w^4, w^8; at most three products deep).
+// PRUNE (W <= 2N/RL): the fftshift crop keeps only last-stage outputs 0 and RL-1, so the
+// last stage forms just those two per block.
 #ifndef WELCH_DIF_PF
-#define WELCH_DIF_PF 16  // values per thread prefetched a segment ahead
+#define WELCH_DIF_PF 16  // values per thread prefetched a segment ahead (N = 4096)
 #endif
-#ifndef WELCH_DIF_B2
-#define WELCH_DIF_B2 1  // stage-2 twiddle bases held in registers (0: re-read per segment)
+#ifndef WELCH_DIF_PF_SMALL
+#define WELCH_DIF_PF_SMALL 8  // the same for N <= 2048
 #endif
 #ifndef WELCH_DIF_WAVES
-#define WELCH_DIF_WAVES 3  // waves per SIMD the registers are cut for (PRUNE; the full form: 2)
+#define WELCH_DIF_WAVES 3  // waves per SIMD the registers are cut for (PRUNE, N = 4096)
 #endif
-__host__ __device__ constexpr int dif_slot(int i) { return i + (i >> 4); }  // conflict-free strides 1, 16
+#ifndef WELCH_DIF_WAVES_SMALL
+#define WELCH_DIF_WAVES_SMALL 3  // the same for N <= 2048 (both forms)
+#endif
+__host__ __device__ constexpr int dif_slot(int i) { return i + (i >> 4); }  // conflict-free strides 1, 16, 17
+
+template <int N>
+struct Dif {
+  static constexpr int LOG2N = N == 1024 ? 10 : N == 2048 ? 11 : N == 4096 ? 12 : N == 8192 ? 13 : 14;
+  static constexpr int T = N / 16;                   // threads per frame
+  static constexpr int P = LOG2N / 4;                // radix-16 stages
+  static constexpr int R0 = N >> (4 * P);            // 1, 2, 4 or 8
+  static constexpr int RL = R0 > 1 ? R0 : 16;        // radix of the last stage
+  static constexpr int PM = R0 > 1 ? P : P - 1;      // radix-16 stages before the last stage
+  static constexpr int FPB = T >= 256 ? 1 : 256 / T; // frames per workgroup
+  static constexpr int NT = T * FPB;                 // threads per workgroup
+  static constexpr int NW = (T + 63) / 64;           // waves per frame
+  static constexpr int SLOTS = dif_slot(N - 1) + 1;  // LDS image per frame (v2f)
+  static constexpr int PF = N <= 2048 ? WELCH_DIF_PF_SMALL : WELCH_DIF_PF;
+  // waves per SIMD the registers are cut for
+  static constexpr int WAVES_PRUNE = N <= 2048 ? WELCH_DIF_WAVES_SMALL : N == 4096 ? WELCH_DIF_WAVES : 2;
+  static constexpr int WAVES_FULL = N <= 2048 ? WELCH_DIF_WAVES_SMALL : 2;
+};
 
 // v[r] *= b^r, r = 1..15, from bp = {b, b^2, b^4, b^8}: each power applied as soon as it
 // is formed (at most eight of them live)
@@ -809,122 +834,194 @@ __device__ __forceinline__ void apply_powers(v2f *v, const v2f *bp) {
   v[15] = cmul(v[15], cmul(w7, bp[3]));
 }
 
-template <bool PRUNE>
-__global__ __launch_bounds__(256, PRUNE ? WELCH_DIF_WAVES : 2) void welch_dif4096_kernel(const v2f *__restrict__ x, int64_t len,
-                                                               const float *__restrict__ win,
-                                                               const v2f *__restrict__ tw, WelchGeom g,
-                                                               float *__restrict__ rows, int frames) {
-  constexpr int N = 4096, T = 256;
-  __shared__ v2f img[dif_slot(N - 1) + 1];
-  __shared__ v2f red[2][4];  // wave partial sums of the segment mean, by segment parity
-  const int t = threadIdx.x;
-  int f = blockIdx.x;
-  if ((frames & 7) == 0 && frames >= 64)  // spread consecutive frames over the 8 XCDs evenly
-    f = (blockIdx.x & 7) * (frames >> 3) + (blockIdx.x >> 3);
-  const v2f *__restrict__ xf = x + (int64_t)f * len;
-  // twiddle bases: stage 1 W_4096^(t m) held, stage 2 W_4096^(16 (t % 16) m) re-read per
-  // segment (L1 hits; WELCH_DIF_B2 holds them too), m = 1, 2, 4, 8
-  v2f b1[4], b2[4];
+// bin of slot q after the last stage (digits reversed)
+template <int N>
+__device__ __forceinline__ int dif_bin(int q) {
+  using D = Dif<N>;
+  int k = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    b1[i] = tw[(t << i) & (N - 1)];
-    if (WELCH_DIF_B2) b2[i] = tw[((16 * (t & 15)) << i) & (N - 1)];
-  }
+  for (int s = 1; s <= D::P; ++s) k += ((q >> (D::LOG2N - 4 * s)) & 15) << (4 * (s - 1));
+  if constexpr (D::R0 > 1) k += (q & (D::R0 - 1)) << (4 * D::P);
+  return k;
+}
 
-  auto load_seg = [&](v2f *dst, int s) {
+template <int N, bool PRUNE>
+__global__ __launch_bounds__(Dif<N>::NT, PRUNE ? Dif<N>::WAVES_PRUNE : Dif<N>::WAVES_FULL)
+void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__restrict__ win,
+                      const v2f *__restrict__ tw, WelchGeom g, float *__restrict__ rows, int frames) {
+  using D = Dif<N>;
+  constexpr int T = D::T, PF = D::PF;
+  extern __shared__ v2f dyn_sh[];
+  __shared__ v2f red[D::FPB][2][D::NW];  // wave partial sums of the segment mean, by parity
+  const int fl = D::FPB == 1 ? 0 : (int)threadIdx.x / T;  // frame within the workgroup
+  int blk = blockIdx.x;
+  const int nblk = (int)gridDim.x;
+  if ((nblk & 7) == 0 && nblk >= 64)  // spread consecutive frames over the 8 XCDs evenly
+    blk = (blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3);
+  // a workgroup's spare frame slots (frames % FPB) recompute the last frame, unwritten
+  const int f = min(blk * D::FPB + fl, frames - 1);
+  const bool owner = blk * D::FPB + fl < frames;
+  v2f *img = dyn_sh + fl * D::SLOTS;
+  const v2f *__restrict__ xf = x + (int64_t)f * len;
+  auto sync = [&]() {
+    if constexpr (D::NW > 1) __syncthreads();
+    else __builtin_amdgcn_wave_barrier();
+  };
+  // twiddle bases of stages 1 and 2 held (stage s: W_N^(j 16^(s-1) m), j = t % (N/16^s),
+  // m = 1, 2, 4, 8); later stages re-read theirs per segment
+  auto base_of = [&](int s, int tt, int i) {
+    const int j = tt & ((N >> (4 * s)) - 1);
+    return tw[(j << (4 * (s - 1) + i)) & (N - 1)];
+  };
+  v2f b1[4], b2[4];
+  {
+    const int t = threadIdx.x % T;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      b1[i] = base_of(1, t, i);
+      b2[i] = D::PM >= 2 ? base_of(2, t, i) : splat(0.f);
+    }
+  }
+  auto load_seg = [&](v2f *dst, int s, int t) {
     const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
 #pragma unroll
-    for (int r = 0; r < WELCH_DIF_PF; ++r) dst[r] = seg[t + T * r];
+    for (int r = 0; r < PF; ++r) dst[r] = seg[t + T * r];
   };
-  // partial sums of segment s: the prefetched values plus a separate pass over the rest
-  auto post_sum = [&](const v2f *v, int slot, int s) {
+  // partial sums of segment s: the prefetched values plus the rest read again
+  auto post_sum = [&](const v2f *v, int slot, int s, int t) {
     v2f sum = splat(0.f);
 #pragma unroll
-    for (int r = 0; r < WELCH_DIF_PF; ++r) sum += v[r];
+    for (int r = 0; r < PF; ++r) sum += v[r];
     const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
 #pragma unroll
-    for (int r = WELCH_DIF_PF; r < 16; ++r) sum += seg[t + T * r];
+    for (int r = PF; r < 16; ++r) sum += seg[t + T * r];
     sum = wave_sum(sum);
-    if ((t & 63) == 0) red[slot][t >> 6] = sum;
+    if ((t & 63) == 0) red[fl][slot][t >> 6] = sum;
   };
-  v2f pf[WELCH_DIF_PF > 0 ? WELCH_DIF_PF : 1];
-  load_seg(pf, 0);
-  post_sum(pf, 0, 0);
-  __syncthreads();
-  float acc[16];
+  v2f pf[PF > 0 ? PF : 1];
+  load_seg(pf, 0, threadIdx.x % T);
+  post_sum(pf, 0, 0, threadIdx.x % T);
+  sync();
+  constexpr int NACC = PRUNE ? 2 * (16 / D::RL) : 16;
+  float acc[NACC];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
 
   for (int s = 0; s < g.nseg; ++s) {
-    // opaque per-segment copies: the twiddle powers and LDS addresses are rebuilt in the
-    // loop rather than hoisted out of it (60 + 48 registers held across the loop)
-    int t = threadIdx.x;
+    // opaque per-segment copies: twiddle powers and LDS addresses are rebuilt in the loop
+    // rather than hoisted out of it (dozens of registers held across the loop)
+    int t = D::FPB == 1 ? (int)threadIdx.x : (int)threadIdx.x % T;
     asm volatile("" : "+v"(t));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       asm volatile("" : "+v"(b1[i]));
-      if (WELCH_DIF_B2) asm volatile("" : "+v"(b2[i]));
-      else b2[i] = tw[((16 * (t & 15)) << i) & (N - 1)];
+      asm volatile("" : "+v"(b2[i]));
     }
     v2f v[16];
-    {  // values [0, WELCH_DIF_PF) were prefetched a segment ahead, the rest load now
+    {  // values [0, PF) were prefetched a segment ahead, the rest load now
       const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = r < WELCH_DIF_PF ? pf[r] : seg[t + T * r];
+      for (int r = 0; r < 16; ++r) v[r] = r < PF ? pf[r] : seg[t + T * r];
     }
     const bool more = s + 1 < g.nseg;
-    if (more) load_seg(pf, s + 1);  // in flight during this segment's transform
+    // (addresses from the loop-invariant thread id: computed once, outside the loop)
+    if (more) load_seg(pf, s + 1, (int)threadIdx.x % T);  // in flight during this segment's transform
     {
-      const v2f mean = (red[s & 1][0] + red[s & 1][1] + red[s & 1][2] + red[s & 1][3]) * (1.f / (float)N);
+      v2f sum = splat(0.f);
+#pragma unroll
+      for (int w = 0; w < D::NW; ++w) sum += red[fl][s & 1][w];
+      const v2f mean = sum * (1.f / (float)N);
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = (v[r] - mean) * win[t + T * r];
     }
-    // stage 1: DFT over n2, twiddle W_4096^(t k0), store at 256 k0 + t
+    // stage 1: DFT16 over the thread's own samples, twiddle, store at t + T k
     dft<16>(v);
     apply_powers(v, b1);
 #pragma unroll
     for (int k = 0; k < 16; ++k) img[dif_slot(T * k + t)] = v[k];
-    __syncthreads();
-    // stage 2: thread (k0, n0); DFT over n1, twiddle W_256^(n0 k1), back to the same slots
-    {
-      const int base = 256 * (t >> 4) + (t & 15);
+    sync();
+    // middle radix-16 stages 2 .. PM
 #pragma unroll
-      for (int n = 0; n < 16; ++n) v[n] = img[dif_slot(base + 16 * n)];
+    for (int st = 2; st <= D::PM; ++st) {
+      const int S16 = N >> (4 * st), M = S16 * 16;
+      const int base = (t / S16) * M + (t & (S16 - 1));
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = img[dif_slot(base + S16 * m)];
       dft<16>(v);
-      apply_powers(v, b2);
+      if (st == 2) {
+        apply_powers(v, b2);
+      } else {
+        v2f bs[4];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) img[dif_slot(base + 16 * k)] = v[k];
-    }
-    if (more) post_sum(pf, (s + 1) & 1, s + 1);  // the next segment's mean, read after two barriers
-    __syncthreads();
-    // stage 3: thread (k0, k1); DFT over n0 -> bins k0 + 16 k1 + 256 k2
-#pragma unroll
-    for (int n = 0; n < 16; ++n) v[n] = img[dif_slot(16 * t + n)];
-    if constexpr (PRUNE) {  // k2 = 0 and k2 = 15 only: X_15 = sum_n v_n W16^(15 n) = sum_n v_n conj(W16^n)
-      v2f a0 = splat(0.f), a15 = splat(0.f);
-#pragma unroll
-      for (int n = 0; n < 16; ++n) {
-        a0 += v[n];
-        const v2f wc = w16(16 - n);  // W16^(-n) = W16^(15 n) (mod 16)
-        a15 += cmul(v[n], wc);
+        for (int i = 0; i < 4; ++i) bs[i] = base_of(st, t, i);
+        apply_powers(v, bs);
       }
-      acc[0] = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, acc[0]));
-      acc[15] = fmaf(a15.x, a15.x, fmaf(a15.y, a15.y, acc[15]));
-    } else {
-      dft<16>(v);
 #pragma unroll
-      for (int k = 0; k < 16; ++k) acc[k] = fmaf(v[k].x, v[k].x, fmaf(v[k].y, v[k].y, acc[k]));
+      for (int k = 0; k < 16; ++k) img[dif_slot(base + S16 * k)] = v[k];
+      if (st == D::PM && more) post_sum(pf, (s + 1) & 1, s + 1, t);  // next mean, read after 2 syncs
+      sync();
     }
-    __syncthreads();  // stage-3 reads done before the next segment's stage-1 stores
-  }
-  float *__restrict__ row = rows + (int64_t)f * g.n_win;
+    if (D::PM < 2 && more) {  // (no middle stage: post before the last barrier instead)
+      post_sum(pf, (s + 1) & 1, s + 1, t);
+      sync();
+    }
+    // last stage: the thread's 16 consecutive slots as 16/RL blocks of RL
 #pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2) {
-    if (PRUNE && k2 != 0 && k2 != 15) continue;
-    const int k = (t >> 4) + 16 * (t & 15) + 256 * k2;
-    const int j = (k + (g.n_win >> 1)) & (N - 1);  // fftshift + crop: row[j] = P[(j - W/2) mod N]
-    if (j < g.n_win) row[j] = 20.f * log10f(acc[k2] * g.scale);
+    for (int m = 0; m < 16; ++m) v[m] = img[dif_slot(16 * t + m)];
+    constexpr int RL = D::RL;
+#pragma unroll
+    for (int u = 0; u < 16 / RL; ++u) {
+      v2f *blkv = v + RL * u;
+      if constexpr (PRUNE) {  // outputs 0 and RL-1: X_(RL-1) = sum_m v_m W_RL^(-m)
+        v2f a0 = splat(0.f), a1 = splat(0.f);
+#pragma unroll
+        for (int m = 0; m < RL; ++m) {
+          a0 += blkv[m];
+          a1 += m == 0 ? blkv[0] : cmul(blkv[m], w16((16 - (16 / RL) * m) & 15));
+        }
+        acc[2 * u] = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, acc[2 * u]));
+        acc[2 * u + 1] = fmaf(a1.x, a1.x, fmaf(a1.y, a1.y, acc[2 * u + 1]));
+      } else {
+        dft<RL>(blkv);
+#pragma unroll
+        for (int m = 0; m < RL; ++m) acc[RL * u + m] = fmaf(blkv[m].x, blkv[m].x, fmaf(blkv[m].y, blkv[m].y, acc[RL * u + m]));
+      }
+    }
+    sync();  // last-stage reads done before the next segment's stage-1 stores
   }
+  const int t = threadIdx.x % T;
+  float *__restrict__ row = rows + (int64_t)f * g.n_win;
+  if (!owner) return;
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) {
+    const int q = PRUNE ? 16 * t + D::RL * (i >> 1) + ((i & 1) ? D::RL - 1 : 0) : 16 * t + i;
+    const int k = dif_bin<N>(q);
+    const int j = (k + (g.n_win >> 1)) & (N - 1);  // fftshift + crop: row[j] = P[(j - W/2) mod N]
+    if (j < g.n_win) row[j] = 20.f * log10f(acc[i] * g.scale);
+  }
+}
+
+template <int N>
+static hipError_t welch_dif_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
+                                   const WelchGeom &g, float *rows, int frames, hipStream_t st) {
+  using D = Dif<N>;
+  const size_t lds = (size_t)D::FPB * D::SLOTS * sizeof(v2f);
+  const bool prune = g.n_win <= 2 * N / D::RL;
+  const void *k = prune ? (const void *)welch_dif_kernel<N, true> : (const void *)welch_dif_kernel<N, false>;
+  static bool attr_set[2] = {false, false};
+  if (lds > 48 * 1024 && !attr_set[prune]) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set[prune] = true;
+  }
+  const dim3 grid((unsigned)((frames + D::FPB - 1) / D::FPB)), block(D::NT);
+  if (prune)
+    hipLaunchKernelGGL((welch_dif_kernel<N, true>), grid, block, lds, st, (const v2f *)x, len, win,
+                       (const v2f *)tw, g, rows, frames);
+  else
+    hipLaunchKernelGGL((welch_dif_kernel<N, false>), grid, block, lds, st, (const v2f *)x, len, win,
+                       (const v2f *)tw, g, rows, frames);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ Welch row, four-step
@@ -1211,17 +1308,23 @@ static hipError_t welch2_launch_t(const float2 *x, int64_t len, const float *win
 #ifndef WELCH_DIF
 #define WELCH_DIF 1
 #endif
+#ifndef WELCH_DIF_MIN
+#define WELCH_DIF_MIN 1024
+#endif
+#ifndef WELCH_DIF_MAX
+#define WELCH_DIF_MAX 8192  // (N = 16384 as one 1024-thread frame spills: four-step by default)
+#endif
 template <int R0>
 static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
                                const WelchGeom &g, float *rows, int frames, hipStream_t st) {
-  if (WELCH_DIF && g.n_fft == 4096 && g.nperseg == 4096) {
-    if (g.n_win <= 512)
-      hipLaunchKernelGGL(welch_dif4096_kernel<true>, dim3(frames), dim3(256), 0, st, (const v2f *)x, len, win,
-                         (const v2f *)tw, g, rows, frames);
-    else
-      hipLaunchKernelGGL(welch_dif4096_kernel<false>, dim3(frames), dim3(256), 0, st, (const v2f *)x, len, win,
-                         (const v2f *)tw, g, rows, frames);
-    return hipGetLastError();
+  if (WELCH_DIF && g.nperseg == g.n_fft && g.n_fft >= WELCH_DIF_MIN && g.n_fft <= WELCH_DIF_MAX) {
+    switch (g.n_fft) {
+      case 1024: return welch_dif_launch<1024>(x, len, win, tw, g, rows, frames, st);
+      case 2048: return welch_dif_launch<2048>(x, len, win, tw, g, rows, frames, st);
+      case 4096: return welch_dif_launch<4096>(x, len, win, tw, g, rows, frames, st);
+      case 8192: return welch_dif_launch<8192>(x, len, win, tw, g, rows, frames, st);
+      default: break;
+    }
   }
   if (WELCH_V2 && g.n_fft <= 4096) return welch2_launch_t<R0, 256>(x, len, win, tw, g, rows, frames, st);
   if (WELCH_V2 && g.n_fft <= 8192) return welch2_launch_t<R0, 512>(x, len, win, tw, g, rows, frames, st);

@@ -154,6 +154,23 @@ def test_batched_frames_vs_oracle(oracle_lib, N, z, L, F):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, z, W), f"frame {f}")
 
 
+@pytest.mark.parametrize("N,z,W,F", [(1024, 4, 256, 5), (1024, 2, 1024, 3), (2048, 8, 256, 3),
+                                      (2048, 2, 2048, 2), (4096, 8, 512, 3), (4096, 4, 1024, 2),
+                                      (8192, 8, 1024, 2), (8192, 2, 4096, 1), (16384, 8, 2048, 1)])
+def test_welch_one_workgroup_forms_vs_oracle(oracle_lib, N, z, W, F):
+    """Welch mode 1 (one workgroup per frame): the in-place DIF kernel for 1024 <= N <= 8192
+    with its pruned (W <= 2N/RL) and full last stage, frames that leave spare slots in a
+    multi-frame workgroup (N = 1024: 4 frames each), and the Stockham kernel at N = 16384."""
+    from pypanadapter_amd import ZoomFFT
+    L = N * z * 6
+    x = _frames(F, L, N, z, W, seed0=8800 + N + z)
+    with ZoomFFT(N, z, 2.4e6, n_win=W) as plan:
+        plan.set_welch(1)
+        rows = plan.rows(x)
+    for f in range(F):
+        assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, z, W), f"N={N} W={W} frame {f}")
+
+
 @pytest.mark.parametrize("block,warm", [(512, 192), (1024, 256), (64, 192), (8192, 128)])
 def test_block_and_warmup_invariance(oracle_lib, block, warm):
     """The result must not depend on how frames are cut into lanes (within the gate)."""
