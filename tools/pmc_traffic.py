@@ -7,8 +7,8 @@ reports exactly half the bytes of a wide coalesced streaming read, so it is doub
 ("fetch x2"); WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Other access
 widths are uncalibrated; both raw and corrected sums are kept.
 
-Per step = (sum over every zfft dispatch) / (number of welch_rows dispatches): each
-process call launches welch_rows exactly once.
+Per step = (sum over every zfft dispatch) / (number of Welch row dispatches): each
+process call launches exactly one of welch_rows / welch_dif / welch4_rows.
 
 usage: tools/pmc_traffic.py <fetch_dir> <write_dir> <frames> <config> [out.json] [schedule]
 """
@@ -44,8 +44,9 @@ def main():
     schedule = sys.argv[6] if len(sys.argv) > 6 else "xa"
     fetch, fc = load(fetch_dir, "FETCH_SIZE")
     write, wc = load(write_dir, "WRITE_SIZE")
-    steps_f = sum(v for k, v in fc.items() if k.startswith("welch_rows"))
-    steps_w = sum(v for k, v in wc.items() if k.startswith("welch_rows"))
+    step_kernel = ("welch_rows", "welch_dif", "welch4_rows")
+    steps_f = sum(v for k, v in fc.items() if k.startswith(step_kernel))
+    steps_w = sum(v for k, v in wc.items() if k.startswith(step_kernel))
     per_kernel = {}
     tot_raw = tot_x2 = 0.0
     for k in sorted(set(fetch) | set(write)):
