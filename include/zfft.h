@@ -117,6 +117,29 @@ int zfft_waterfall_read(zfft_plan *plan, float *img_out /* host, H*n_win */);
 int zfft_waterfall_reset(zfft_plan *plan, int32_t scroll);
 int zfft_waterfall_shape(const zfft_plan *plan, int32_t *rows, int32_t *cols);
 
+/* On-device waterfall rendering.  The reference hands img_array.T to a
+ * pyqtgraph ImageItem with a 256-entry colormap LUT and fixed levels (Waterfall.__init__ /
+ * lookuptable / newlevel / autolevel, pypanadapter_spectrum.py:1579-1623, 1667-1685); these
+ * produce the RGBA pixels that ImageItem draws for the ring image, on the device:
+ *   pixel = LUT[clip(trunc((v - min) * 256 / (max - min)), 0, 255)], alpha 255
+ * (pyqtgraph makeARGB / rescaleData / applyLookupTable), rows in zfft_waterfall_read order.
+ * Colormaps 'Default', 'Matrix', 'Red Green', 'Tropical' (S:1580-1585; any other name ->
+ * 'Default', S:1613-1616); the LUT is linspace(0, 1, 256) through the stops, channels
+ * truncated to uint8 (ColorMap.getLookupTable(0, 1, 256)).  'Default' carries the
+ * reference's out-of-range stop value 2020 as numpy < 2 stored it in a uint8 (2020 mod 256
+ * = 228; numpy 2 raises OverflowError there).  Initial levels -220 .. -120 (S:1593-1598).
+ * autolevel sets the levels to the 2nd and 98th percentiles (numpy 'linear') of the pixels
+ * below 0 -- what S:1676 computes; the reference then assigns them to unused attributes,
+ * so its autolevel never changes the levels (a bug, SURVEY §8 a-6 note). */
+int zfft_colormap_lut(const char *name, uint8_t *lut_rgba /* 256*4; no plan, no GPU */);
+int zfft_waterfall_colormap(zfft_plan *plan, const char *name);
+int zfft_waterfall_levels(zfft_plan *plan, double minlev, double maxlev);
+int zfft_waterfall_get_levels(const zfft_plan *plan, double *minlev, double *maxlev);
+int zfft_waterfall_autolevel(zfft_plan *plan, double *minlev, double *maxlev);
+int zfft_waterfall_render(zfft_plan *plan, uint8_t *rgba_out /* host, H*n_win*4 */);
+int zfft_waterfall_render_device(zfft_plan *plan, uint8_t *d_rgba /* H*n_win*4 */,
+                                 void *hip_stream);
+
 /* Native window generation (fp64), for tests and for callers without scipy. */
 int zfft_window_values(int32_t kind, const double *param, int32_t length, double *out);
 

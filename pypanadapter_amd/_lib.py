@@ -56,6 +56,9 @@ EXPORTS = [
     "zfft_waterfall_read", "zfft_waterfall_reset", "zfft_waterfall_shape", "zfft_window_values",
     "zfft_plan_tune", "zfft_plan_timing", "zfft_plan_timings", "zfft_plan_timing_names",
     "zfft_plan_path", "zfft_plan_welch", "zfft_last_error",
+    "zfft_colormap_lut", "zfft_waterfall_colormap", "zfft_waterfall_levels",
+    "zfft_waterfall_get_levels", "zfft_waterfall_autolevel", "zfft_waterfall_render",
+    "zfft_waterfall_render_device",
     "zfft_device_count", "zfft_version",
 ]
 
@@ -119,6 +122,13 @@ def load(path: str = ""):
         "zfft_plan_path": (ctypes.c_int, [P, I32]),
         "zfft_plan_welch": (ctypes.c_int, [P, I32]),
         "zfft_last_error": (ctypes.c_char_p, []),
+        "zfft_colormap_lut": (ctypes.c_int, [ctypes.c_char_p, P]),
+        "zfft_waterfall_colormap": (ctypes.c_int, [P, ctypes.c_char_p]),
+        "zfft_waterfall_levels": (ctypes.c_int, [P, D, D]),
+        "zfft_waterfall_get_levels": (ctypes.c_int, [P, ctypes.POINTER(D), ctypes.POINTER(D)]),
+        "zfft_waterfall_autolevel": (ctypes.c_int, [P, ctypes.POINTER(D), ctypes.POINTER(D)]),
+        "zfft_waterfall_render": (ctypes.c_int, [P, P]),
+        "zfft_waterfall_render_device": (ctypes.c_int, [P, P, P]),
         "zfft_device_count": (ctypes.c_int, []),
         "zfft_version": (ctypes.c_int, []),
     }
@@ -126,7 +136,6 @@ def load(path: str = ""):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _ = D
     _lib = lib
     return lib
 

@@ -301,7 +301,7 @@ __device__ __forceinline__ void fold_entering(Md &m, const Md &in, CT tab, bool 
 
 // Diagnostic build only (-DXA_STAMPS=1, tools/build_variants.py): per-phase s_memtime
 // sums of every wave, read back with zfft_debug_xa_stamps; no stamp exists otherwise.
-constexpr int kStampSegs = 10;
+[[maybe_unused]] constexpr int kStampSegs = 10;
 #if XA_STAMPS
 __device__ unsigned long long g_xa_stamps[kStampSegs + 1];
 #define XA_STAMP(i)                                                                   \

@@ -157,6 +157,14 @@ hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,
                                  hipStream_t st);
 hipError_t launch_waterfall_read(const float *ring, int H, int W, int64_t off, float *img,
                                  hipStream_t st);
+// waterfall rendering: RGBA8 pixels of the ring in read order
+hipError_t launch_waterfall_render(const float *ring, int H, int W, int64_t off, const void *lut,
+                                   double lo, double scale, void *out, hipStream_t st);
+// autolevel order statistics of the pixels < 0: top-16-bit key histogram (65536 bins), then
+// the low-16-bit histograms inside nbins (<= 4) chosen top bins
+hipError_t launch_autolevel_hist_hi(const float *ring, int64_t n, unsigned *hist, hipStream_t st);
+hipError_t launch_autolevel_hist_lo(const float *ring, int64_t n, const unsigned *bins, int nbins,
+                                    unsigned *hist, hipStream_t st);
 // out[f][i] = in(f, i) (* lo[i] when lo) as complex64, natural layout, frames x len.
 hipError_t launch_ingest(const InDesc &in, const float2 *lo, float2 *out, int frames,
                          hipStream_t st);

@@ -16,6 +16,7 @@
 // rounding, tools/sim_blocked.py); blocks at the frame edges run scipy's exact
 // initial conditions (zi * ext[0] forward, zi * y[-1] backward).  I and Q share the real
 // coefficients, so each lane carries them as one packed float2 (v_pk_fma_f32).
+#include <algorithm>
 #include <type_traits>
 
 #include "zfft_device.h"
@@ -1175,6 +1176,48 @@ __global__ __launch_bounds__(1024) void waterfall_push_kernel(float *ring, int H
   }
 }
 
+// Waterfall rendering: pyqtgraph makeARGB of the ring image, pixel order as
+// waterfall_read.  idx = clip((v - lo) * scale, 0, 255) truncated (rescaleData then
+// astype(uint8)), computed in fp64 as numpy does on the float64 image; NaN -> alpha 0.
+__global__ void waterfall_render_kernel(const float *__restrict__ ring, int H, int W, int off,
+                                        const uchar4 *__restrict__ lut, double lo, double scale,
+                                        uchar4 *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)H * W) return;
+  const int r = (int)(i / W), xcol = (int)(i % W);
+  const float v = ring[(int64_t)((r + off) % H) * W + xcol];
+  double t = ((double)v - lo) * scale;
+  t = t < 0.0 ? 0.0 : (t > 255.0 ? 255.0 : t);
+  uchar4 c = lut[v == v ? (int)t : 0];
+  if (v != v) c.w = 0;
+  out[i] = c;
+}
+
+// Autolevel order statistics of the ring pixels below 0: keys are the float bits made
+// order-preserving (negative floats: all bits flipped), counted in 65536 bins of the top 16
+// bits, then -- inside the bins that hold the wanted ranks -- of the low 16 bits.
+__device__ __forceinline__ uint32_t neg_key(float v) { return ~__float_as_uint(v); }
+__global__ void autolevel_hist_hi_kernel(const float *__restrict__ ring, int64_t n,
+                                         unsigned *__restrict__ hist) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = ring[i];
+    if (v < 0.f) atomicAdd(&hist[neg_key(v) >> 16], 1u);
+  }
+}
+__global__ void autolevel_hist_lo_kernel(const float *__restrict__ ring, int64_t n,
+                                         const unsigned *__restrict__ bins, int nbins,
+                                         unsigned *__restrict__ hist) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = ring[i];
+    if (!(v < 0.f)) continue;
+    const uint32_t k = neg_key(v);
+    for (int b = 0; b < nbins; ++b)
+      if ((k >> 16) == bins[b]) atomicAdd(&hist[b * 65536 + (k & 0xFFFF)], 1u);
+  }
+}
+
 __global__ void waterfall_read_kernel(const float *__restrict__ ring, int H, int W, int off,
                                       float *__restrict__ img) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1395,6 +1438,28 @@ hipError_t launch_waterfall_read(const float *ring, int H, int W, int64_t off, f
                                  hipStream_t st) {
   hipLaunchKernelGGL(waterfall_read_kernel, dim3(nblocks((int64_t)H * W, 256)), dim3(256), 0, st,
                      ring, H, W, (int)(off % H), img);
+  return hipGetLastError();
+}
+
+hipError_t launch_waterfall_render(const float *ring, int H, int W, int64_t off, const void *lut,
+                                   double lo, double scale, void *out, hipStream_t st) {
+  const int64_t total = (int64_t)H * W;
+  hipLaunchKernelGGL(waterfall_render_kernel, dim3(nblocks(total, 256)), dim3(256), 0, st, ring, H,
+                     W, (int)off, (const uchar4 *)lut, lo, scale, (uchar4 *)out);
+  return hipGetLastError();
+}
+
+hipError_t launch_autolevel_hist_hi(const float *ring, int64_t n, unsigned *hist, hipStream_t st) {
+  const unsigned blocks = (unsigned)std::min<int64_t>(nblocks(n, 256), 4096);
+  hipLaunchKernelGGL(autolevel_hist_hi_kernel, dim3(blocks), dim3(256), 0, st, ring, n, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_autolevel_hist_lo(const float *ring, int64_t n, const unsigned *bins, int nbins,
+                                    unsigned *hist, hipStream_t st) {
+  const unsigned blocks = (unsigned)std::min<int64_t>(nblocks(n, 256), 4096);
+  hipLaunchKernelGGL(autolevel_hist_lo_kernel, dim3(blocks), dim3(256), 0, st, ring, n, bins, nbins,
+                     hist);
   return hipGetLastError();
 }
 

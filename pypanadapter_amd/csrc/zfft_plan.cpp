@@ -351,6 +351,53 @@ bool xa_build_tables(XaTab &X) {
   return true;
 }
 
+// ---- waterfall colormaps (Waterfall.Colors / lookuptable, S:1580-1585, 1613-1623) ----
+// pg.ColorMap(pos, color).getLookupTable(0.0, 1.0, 256): x = linspace(0, 1, 256), each
+// channel np.interp(x, pos, color), truncated to uint8; the maps are opaque, so the LUT has
+// no alpha channel and makeARGB draws alpha 255.  'Default' keeps the reference's stop
+// value 2020 as a numpy < 2 uint8 array stored it (2020 mod 256 = 228).
+struct ColorStops {
+  const char *name;
+  int n;
+  double pos[6];
+  int rgba[6][4];
+};
+const ColorStops kColormaps[] = {
+    {"Default", 3, {0.0, 0.4, 1.0}, {{0, 0, 90, 255}, {200, 2020 % 256, 0, 255}, {255, 0, 0, 255}}},
+    {"Matrix", 2, {0.0, 1.0}, {{0, 0, 0, 255}, {0, 255, 0, 255}}},
+    {"Red Green", 3, {0.0, 0.5, 1.0}, {{0, 0, 0, 255}, {0, 255, 0, 255}, {255, 0, 0, 255}}},
+    {"Tropical", 6, {0.0, 0.2, 0.4, 0.6, 0.8, 1.0},
+     {{68, 40, 153, 255}, {222, 68, 252, 255}, {252, 38, 99, 255}, {252, 181, 38, 255},
+      {86, 235, 49, 255}, {3, 71, 7, 255}}},
+};
+
+// np.interp(x, xp, fp) for increasing xp (numpy/core/src/multiarray/compiled_base.c)
+double np_interp(double x, const double *xp, const double *fp, int n) {
+  if (x <= xp[0]) return fp[0];
+  if (x >= xp[n - 1]) return fp[n - 1];
+  int j = 0;
+  while (j + 1 < n && xp[j + 1] <= x) ++j;
+  if (x == xp[j]) return fp[j];
+  const double slope = (fp[j + 1] - fp[j]) / (xp[j + 1] - xp[j]);
+  return slope * (x - xp[j]) + fp[j];
+}
+
+void build_lut(const char *name, uint8_t *lut) {
+  const ColorStops *cm = &kColormaps[0];  // any other name -> 'Default' (S:1613-1614)
+  for (const ColorStops &c : kColormaps)
+    if (name && std::strcmp(name, c.name) == 0) cm = &c;
+  const double step = 1.0 / 255.0;  // np.linspace(0, 1, 256): arange * step, last = stop
+  for (int i = 0; i < 256; ++i) {
+    const double x = i == 255 ? 1.0 : (double)i * step;
+    for (int ch = 0; ch < 3; ++ch) {
+      double fp[6];
+      for (int k = 0; k < cm->n; ++k) fp[k] = (double)cm->rgba[k][ch];
+      lut[4 * i + ch] = (uint8_t)np_interp(x, cm->pos, fp, cm->n);  // astype(ubyte): truncation
+    }
+    lut[4 * i + 3] = 255;
+  }
+}
+
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -416,6 +463,13 @@ struct zfft_plan {
                 // 4 XA tiles (all-pole + FIR + half-rate all-pole)
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
   DevBuf edge, xk, xt_tab, xa_tab, tws, means, z4;
+  // waterfall rendering: colormap LUT (host copy + device), levels
+  uint8_t lut[256 * 4] = {};
+  bool lut_ready = false;         // lut holds the chosen map (built on first use)
+  bool lut_uploaded = false;      // lut_d holds lut
+  std::string cmap = "Default";
+  double lev_lo = -220.0, lev_hi = -120.0;  // Waterfall.__init__ (S:1593-1598)
+  DevBuf lut_d, rgba, al_hist, al_bins;
 };
 
 namespace {
@@ -1115,6 +1169,168 @@ int zfft_waterfall_read(zfft_plan *p, float *img_out) {
                        hipMemcpyDeviceToHost, p->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
   return e == hipSuccess ? ZFFT_OK : hip_fail(e, "waterfall read");
+}
+
+int zfft_colormap_lut(const char *name, uint8_t *lut_rgba) {
+  if (!lut_rgba) return fail(ZFFT_EINVAL, "null output");
+  build_lut(name, lut_rgba);
+  return ZFFT_OK;
+}
+
+int zfft_waterfall_colormap(zfft_plan *p, const char *name) {
+  int rc = enter(p);
+  if (rc) return rc;
+  p->cmap = name ? name : "Default";
+  p->lut_ready = p->lut_uploaded = false;
+  return ZFFT_OK;
+}
+
+int zfft_waterfall_levels(zfft_plan *p, double minlev, double maxlev) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!std::isfinite(minlev) || !std::isfinite(maxlev)) return fail(ZFFT_EINVAL, "levels must be finite");
+  p->lev_lo = minlev;
+  p->lev_hi = maxlev;
+  return ZFFT_OK;
+}
+
+int zfft_waterfall_get_levels(const zfft_plan *p, double *minlev, double *maxlev) {
+  if (!p || !minlev || !maxlev) return fail(ZFFT_EINVAL, "null argument");
+  *minlev = p->lev_lo;
+  *maxlev = p->lev_hi;
+  return ZFFT_OK;
+}
+
+int zfft_waterfall_render_device(zfft_plan *p, uint8_t *d_rgba, void *hip_stream) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!d_rgba) return fail(ZFFT_EINVAL, "null output");
+  rc = ensure_waterfall(p);
+  if (rc) return rc;
+  hipError_t e = hipSuccess;
+  if (!p->lut_ready) {
+    build_lut(p->cmap.c_str(), p->lut);
+    p->lut_ready = true;
+  }
+  if (!p->lut_uploaded) {
+    e = p->lut_d.ensure(sizeof(p->lut));
+    if (e == hipSuccess) e = hipMemcpyAsync(p->lut_d.p, p->lut, sizeof(p->lut), hipMemcpyHostToDevice, p->stream);
+    if (e != hipSuccess) return hip_fail(e, "LUT upload");
+    p->lut_uploaded = true;
+  }
+  hipStream_t st = pick_stream(p, hip_stream);
+  if (st != p->stream) {  // ring init / LUT upload were enqueued on the plan stream
+    e = hipStreamSynchronize(p->stream);
+    if (e != hipSuccess) return hip_fail(e, "sync");
+  }
+  // makeARGB levels (pyqtgraph functions.py): equal levels -> max = nextafter(max, 2 max);
+  // scale = lut size / (max - min) (1 when the range is 0)
+  double lo = p->lev_lo, hi = p->lev_hi;
+  if (lo == hi) hi = std::nextafter(hi, 2.0 * hi);
+  double rng = hi - lo;
+  if (rng == 0.0) rng = 1.0;
+  e = launch_waterfall_render(p->ring.as<float>(), p->H, p->W, p->off, p->lut_d.p, lo, 256.0 / rng,
+                              d_rgba, st);
+  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "waterfall render");
+}
+
+int zfft_waterfall_render(zfft_plan *p, uint8_t *rgba_out) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!rgba_out) return fail(ZFFT_EINVAL, "null output");
+  rc = ensure_waterfall(p);
+  if (rc) return rc;
+  const size_t bytes = (size_t)p->H * p->W * 4;
+  hipError_t e = p->rgba.ensure(bytes);
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "render buffer allocation failed");
+  rc = zfft_waterfall_render_device(p, p->rgba.as<uint8_t>(), p->stream);
+  if (rc) return rc;
+  e = hipMemcpyAsync(rgba_out, p->rgba.p, bytes, hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "render copy");
+}
+
+int zfft_waterfall_autolevel(zfft_plan *p, double *minlev, double *maxlev) {
+  int rc = enter(p);
+  if (rc) return rc;
+  rc = ensure_waterfall(p);
+  if (rc) return rc;
+  const int64_t n = (int64_t)p->H * p->W;
+  hipError_t e = p->al_hist.ensure(4 * 65536 * sizeof(unsigned));
+  if (e == hipSuccess) e = p->al_bins.ensure(4 * sizeof(unsigned));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "autolevel workspace allocation failed");
+  // pass 1: counts per top-16-bit key of the pixels < 0
+  std::vector<unsigned> h1(65536);
+  e = hipMemsetAsync(p->al_hist.p, 0, 65536 * sizeof(unsigned), p->stream);
+  if (e == hipSuccess) e = launch_autolevel_hist_hi(p->ring.as<float>(), n, p->al_hist.as<unsigned>(), p->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h1.data(), p->al_hist.p, 65536 * sizeof(unsigned), hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+  if (e != hipSuccess) return hip_fail(e, "autolevel pass 1");
+  int64_t cnt = 0;
+  for (unsigned c : h1) cnt += c;
+  if (cnt == 0) return fail(ZFFT_EINVAL, "autolevel: no pixel below 0");  // np.percentile of an empty array raises
+  // numpy percentile, method 'linear': virtual index (n-1) q, q = p/100; the order
+  // statistics at floor and floor+1 (clipped to n-1)
+  const double qs[2] = {2.0 / 100.0, 98.0 / 100.0};
+  double vi[2];
+  int64_t ranks[4];
+  for (int k = 0; k < 2; ++k) {
+    vi[k] = (double)(cnt - 1) * qs[k];
+    const int64_t prev = (int64_t)std::floor(vi[k]);
+    ranks[2 * k] = std::min<int64_t>(std::max<int64_t>(prev, 0), cnt - 1);
+    ranks[2 * k + 1] = std::min<int64_t>(std::max<int64_t>(prev + 1, 0), cnt - 1);
+  }
+  // the top bin and the rank inside it of each wanted rank
+  unsigned bin_of[4];
+  int64_t within[4];
+  for (int r = 0; r < 4; ++r) {
+    int64_t acc = 0;
+    unsigned b = 0;
+    while (acc + h1[b] <= ranks[r]) acc += h1[b++];
+    bin_of[r] = b;
+    within[r] = ranks[r] - acc;
+  }
+  unsigned bins[4];
+  int nb = 0, slot[4];
+  for (int r = 0; r < 4; ++r) {
+    int j = 0;
+    while (j < nb && bins[j] != bin_of[r]) ++j;
+    if (j == nb) bins[nb++] = bin_of[r];
+    slot[r] = j;
+  }
+  std::vector<unsigned> h2((size_t)nb * 65536);
+  e = hipMemcpyAsync(p->al_bins.p, bins, nb * sizeof(unsigned), hipMemcpyHostToDevice, p->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(p->al_hist.p, 0, (size_t)nb * 65536 * sizeof(unsigned), p->stream);
+  if (e == hipSuccess)
+    e = launch_autolevel_hist_lo(p->ring.as<float>(), n, p->al_bins.as<unsigned>(), nb, p->al_hist.as<unsigned>(), p->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h2.data(), p->al_hist.p, (size_t)nb * 65536 * sizeof(unsigned), hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+  if (e != hipSuccess) return hip_fail(e, "autolevel pass 2");
+  double val[4];
+  for (int r = 0; r < 4; ++r) {
+    const unsigned *hb = h2.data() + (size_t)slot[r] * 65536;
+    int64_t acc = 0;
+    unsigned lo16 = 0;
+    while (acc + hb[lo16] <= within[r]) acc += hb[lo16++];
+    const uint32_t key = (bin_of[r] << 16) | lo16;
+    uint32_t bits = ~key;  // neg_key inverse
+    float f;
+    std::memcpy(&f, &bits, 4);
+    val[r] = (double)f;
+  }
+  // numpy _lerp(a, b, t): a + (b - a) t, or b - (b - a)(1 - t) when t >= 0.5
+  double lev[2];
+  for (int k = 0; k < 2; ++k) {
+    const double a = val[2 * k], b = val[2 * k + 1];
+    const double t = vi[k] - std::floor(vi[k]);
+    const double d = b - a;
+    lev[k] = t >= 0.5 ? b - d * (1.0 - t) : a + d * t;
+  }
+  p->lev_lo = lev[0];
+  p->lev_hi = lev[1];
+  if (minlev) *minlev = lev[0];
+  if (maxlev) *maxlev = lev[1];
+  return ZFFT_OK;
 }
 
 }  // extern "C"

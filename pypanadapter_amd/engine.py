@@ -197,7 +197,52 @@ class ZoomFFT:
 
     def waterfall_reset(self, scroll: int) -> None:
         check(self.lib.zfft_waterfall_reset(self._plan, int(scroll)), "zfft_waterfall_reset")
+
+    # ---------------------------------------------------------------- rendering (§8f-2)
+    def waterfall_colormap(self, name: str) -> None:
+        """Waterfall.lookuptable (S:1611-1623): unknown names fall back to 'Default'."""
+        check(self.lib.zfft_waterfall_colormap(self._plan, str(name).encode()), "zfft_waterfall_colormap")
+
+    def waterfall_levels(self, low: float | None = None, high: float | None = None):
+        """Waterfall.newlevel (S:1680-1684) when given; returns the current (low, high)."""
+        if low is not None:
+            check(self.lib.zfft_waterfall_levels(self._plan, float(low), float(high)),
+                  "zfft_waterfall_levels")
+        lo, hi = ctypes.c_double(), ctypes.c_double()
+        check(self.lib.zfft_waterfall_get_levels(self._plan, ctypes.byref(lo), ctypes.byref(hi)),
+              "zfft_waterfall_get_levels")
+        return lo.value, hi.value
+
+    def waterfall_autolevel(self):
+        """Waterfall.autolevel (S:1667-1678) as intended: levels = percentiles 2, 98 of the
+        pixels below 0, computed on the device; returns (low, high)."""
+        lo, hi = ctypes.c_double(), ctypes.c_double()
+        check(self.lib.zfft_waterfall_autolevel(self._plan, ctypes.byref(lo), ctypes.byref(hi)),
+              "zfft_waterfall_autolevel")
+        return lo.value, hi.value
+
+    def waterfall_render(self) -> np.ndarray:
+        """RGBA uint8 (H, W, 4): the pixels pyqtgraph's ImageItem draws for the ring image."""
+        h, w = self.waterfall_shape()
+        out = np.empty((h, w, 4), dtype=np.uint8)
+        check(self.lib.zfft_waterfall_render(self._plan, out.ctypes.data_as(ctypes.c_void_p)),
+              "zfft_waterfall_render")
+        return out
+
+    def waterfall_render_device(self, d_rgba_ptr: int, stream: int = 0) -> None:
+        check(self.lib.zfft_waterfall_render_device(self._plan, ctypes.c_void_p(d_rgba_ptr),
+                                                    ctypes.c_void_p(stream)),
+              "zfft_waterfall_render_device")
         self.scroll = int(scroll)
+
+
+def colormap_lut(name: str) -> np.ndarray:
+    """The 256 x 4 RGBA lookup table of a Waterfall colormap (host-side, no GPU needed)."""
+    lib = _lib.load()
+    out = np.empty((256, 4), dtype=np.uint8)
+    check(lib.zfft_colormap_lut(str(name).encode(), out.ctypes.data_as(ctypes.c_void_p)),
+          "zfft_colormap_lut")
+    return out
 
 
 def native_window(window, length: int) -> np.ndarray:

@@ -103,6 +103,8 @@ class Waterfall:
         self.fs = fs
         self.fftwidth = 0
         self._plan: ZoomFFT | None = None
+        self._cmap = "Default"
+        self._levels = (-220.0, -120.0)  # Waterfall.__init__ (S:1593-1598)
 
     def _ensure(self, width: int):
         if width != self.fftwidth or self._plan is None:
@@ -111,6 +113,8 @@ class Waterfall:
             n_fft = 1 << max(5, (width - 1).bit_length())
             self._plan = ZoomFFT(n_fft, 1, self.fs, n_win=width, scroll=self.scroll,
                                  device=self.device)
+            self._plan.waterfall_colormap(self._cmap)
+            self._plan.waterfall_levels(*self._levels)
             self.fftwidth = width
 
     def init_image(self):
@@ -134,3 +138,37 @@ class Waterfall:
         if self._plan is None:
             raise AttributeError("img_array is created by the first image_update")
         return self._plan.waterfall_image().astype(np.float64)
+
+    # ---- rendering: Waterfall.lookuptable / newlevel / autolevel, and the
+    #      RGBA image pyqtgraph's ImageItem draws from img_array (S:1579-1623, 1667-1685)
+    Colors = ("Default", "Matrix", "Red Green", "Tropical")
+
+    def _need_plan(self):
+        if self._plan is None:
+            raise AttributeError("the waterfall image is created by the first image_update")
+        return self._plan
+
+    def lookuptable(self, choice: str) -> None:
+        self._cmap = choice if choice in self.Colors else "Default"  # S:1613-1614
+        if self._plan is not None:
+            self._plan.waterfall_colormap(self._cmap)
+
+    def newlevel(self, low: float, high: float):
+        self._levels = (float(low), float(high))
+        if self._plan is not None:
+            self._plan.waterfall_levels(low, high)
+        return low, high
+
+    def autolevel(self):
+        """Levels from the 2nd / 98th percentiles of the pixels below 0 (what S:1676
+        computes; the reference stores them in unused attributes, so its button is a no-op)."""
+        self._levels = self._need_plan().waterfall_autolevel()
+        return self._levels
+
+    @property
+    def levels(self):
+        return self._plan.waterfall_levels() if self._plan is not None else self._levels
+
+    def render(self) -> np.ndarray:
+        """RGBA uint8 (H, W, 4) in img_array's row order."""
+        return self._need_plan().waterfall_render()

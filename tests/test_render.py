@@ -1,0 +1,101 @@
+"""On-device waterfall rendering: colormap LUTs, levels, autolevel, RGBA.
+
+Oracle: oracle/render.py, a numpy restatement of the reference's Waterfall colormap /
+levels / autolevel (pypanadapter_spectrum.py:1579-1623, 1667-1685) and of what pyqtgraph
+draws from them.  pyqtgraph is absent from this image, so parity with pyqtgraph itself is
+unpinned; the device path must equal the restatement bit for bit."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import render as rr
+
+NAMES = ["Default", "Matrix", "Red Green", "Tropical", "no such map"]
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_colormap_lut_matches_restatement(zfft_lib, name):
+    out = np.empty((256, 4), dtype=np.uint8)
+    assert zfft_lib.zfft_colormap_lut(name.encode(), out.ctypes.data_as(ctypes.c_void_p)) == 0
+    np.testing.assert_array_equal(out, rr.lookup_table(name))
+
+
+def test_restatement_facts():
+    """Stops land where Waterfall.Colors puts them; 'Default' carries the numpy<2 wrap."""
+    d = rr.lookup_table("Default")
+    np.testing.assert_array_equal(d[0], [0, 0, 90, 255])
+    np.testing.assert_array_equal(d[255], [255, 0, 0, 255])
+    assert 2020 % 256 == 228 and d[102, 1] > 200  # near pos 0.4: the wrapped 228 green
+    np.testing.assert_array_equal(rr.lookup_table("no such map"), d)
+    img = np.array([[-500.0, 0.0, -220.0, -120.0, -170.0, np.float32(-119.9)]])
+    px = rr.render(img, rr.lookup_table("Matrix"), (-220, -120))
+    np.testing.assert_array_equal(px[0, :, 1], [0, 255, 0, 255, 128, 255])
+
+
+def _filled_plan(W=512, scroll=1, seed=0, rows=None):
+    from pypanadapter_amd import ZoomFFT
+    plan = ZoomFFT(max(1024, W), 2, 2.4e6, n_win=W, scroll=scroll)
+    rng = np.random.default_rng(seed)
+    H = W // 4
+    for _ in range(rows if rows is not None else H // 2):
+        r = (-170 + 40 * rng.standard_normal(W)).astype(np.float32)
+        r[0] = r[W // 2] = r[W - 1] = 0
+        plan.waterfall_push(r)
+    return plan
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,levels", [("Default", None), ("Tropical", (-200.0, -140.0)),
+                                         ("Red Green", (-150.0, -150.0)), ("Matrix", (-260.5, -90.25))])
+def test_render_matches_restatement(name, levels):
+    plan = _filled_plan(seed=len(name))
+    try:
+        plan.waterfall_colormap(name)
+        if levels is not None:
+            plan.waterfall_levels(*levels)
+        lv = plan.waterfall_levels()
+        assert lv == (levels if levels is not None else (-220.0, -120.0))
+        px = plan.waterfall_render()
+        img = plan.waterfall_image().astype(np.float64)
+        np.testing.assert_array_equal(px, rr.render(img, rr.lookup_table(name), lv))
+    finally:
+        plan.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,rows,scroll", [(512, 64, 1), (512, 200, -1), (64, 3, 1), (2048, 40, 1)])
+def test_autolevel_matches_numpy_percentile(W, rows, scroll):
+    plan = _filled_plan(W=W, scroll=scroll, seed=W + rows, rows=rows)
+    try:
+        got = plan.waterfall_autolevel()
+        img = plan.waterfall_image().astype(np.float64)
+        assert got == rr.autolevel(img)  # bit-exact: same order statistics, numpy's lerp
+        assert plan.waterfall_levels() == got
+        np.testing.assert_array_equal(plan.waterfall_render(),
+                                      rr.render(img, rr.lookup_table("Default"), got))
+    finally:
+        plan.close()
+
+
+@pytest.mark.gpu
+def test_waterfall_facade_rendering():
+    """Waterfall.lookuptable / newlevel / autolevel / render on the facade, through a width
+    change (init_image) that keeps the chosen map and levels."""
+    from pypanadapter_amd import Waterfall
+    wf = Waterfall(scroll=1)
+    wf.lookuptable("Tropical")
+    wf.newlevel(-210.0, -130.0)
+    rng = np.random.default_rng(5)
+    for W in (256, 512):
+        for _ in range(20):
+            wf.image_update((-170 + 30 * rng.standard_normal(W)).astype(np.float32))
+        assert wf.levels == (-210.0, -130.0)
+        img = wf.img_array
+        np.testing.assert_array_equal(wf.render(), rr.render(img, rr.lookup_table("Tropical"),
+                                                             (-210.0, -130.0)))
+    lv = wf.autolevel()
+    assert lv == rr.autolevel(wf.img_array)
+    np.testing.assert_array_equal(wf.render(), rr.render(wf.img_array, rr.lookup_table("Tropical"), lv))
+    wf.lookuptable("nope")
+    np.testing.assert_array_equal(wf.render(), rr.render(wf.img_array, rr.lookup_table("Default"), lv))
