@@ -91,6 +91,7 @@ typedef struct zfft_plan zfft_plan;
  * scipy rejects a window longer than the input). */
 int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_plan **out);
 int zfft_plan_destroy(zfft_plan *plan);
+int zfft_plan_config(const zfft_plan *plan, zfft_config *out);  /* the configuration in use */
 
 /* Host-buffer path: n_frames frames of n_samples IQ each (frame-major), rows_out holds
  * n_frames*n_win floats.  Synchronous.  PCIe-inclusive. */
@@ -116,6 +117,27 @@ int zfft_waterfall_push_device(zfft_plan *plan, const float *d_rows, int32_t cou
 int zfft_waterfall_read(zfft_plan *plan, float *img_out /* host, H*n_win */);
 int zfft_waterfall_reset(zfft_plan *plan, int32_t scroll);
 int zfft_waterfall_shape(const zfft_plan *plan, int32_t *rows, int32_t *cols);
+
+/* Host IQ accumulation ring: pypanadapter_thread.py's `Data` (T:1400-1483)
+ * between the reader thread and the PSD worker, in pinned host memory.  capacity =
+ * 16 * chunk_size (T:1409); zfft_ring_add = Data.add without the pacing sleep: a chunk that
+ * would run past the end is written at 0 instead (T:1437-1442), real_size is the high-water
+ * mark and total_size the samples added since the last drain; zfft_ring_take =
+ * get_data_start / data[:real_size] / get_data_end (T:1516-1520): it returns that frame
+ * (after a fold-back: newest chunks first, as the reference reads it) and resets the
+ * counts.  Two buffers alternate, so the returned frame stays intact until the next take
+ * while add() continues (the reference's consumer keeps a view the reader may overwrite).
+ * zfft_ring_process = PSD.update (T:1513-1548): take, skip frames shorter than n_fft
+ * (*produced = 0), else one row through zfft_process from the pinned frame.  Thread-safe:
+ * one producer and one consumer. */
+typedef struct zfft_ring zfft_ring;
+int zfft_ring_create(int64_t chunk_size, int32_t in_dtype, zfft_ring **out);
+int zfft_ring_destroy(zfft_ring *ring);
+int zfft_ring_add(zfft_ring *ring, const void *chunk, int64_t n_samples);
+int zfft_ring_state(zfft_ring *ring, int64_t *size, int64_t *real_size, int64_t *total_size);
+int zfft_ring_take(zfft_ring *ring, const void **frame, int64_t *n_samples, int64_t *total_size);
+int zfft_ring_process(zfft_ring *ring, zfft_plan *plan, float *row_out /* host, n_win */,
+                      int32_t *produced);
 
 /* On-device waterfall rendering.  The reference hands img_array.T to a
  * pyqtgraph ImageItem with a 256-entry colormap LUT and fixed levels (Waterfall.__init__ /

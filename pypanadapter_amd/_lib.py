@@ -56,6 +56,8 @@ EXPORTS = [
     "zfft_waterfall_read", "zfft_waterfall_reset", "zfft_waterfall_shape", "zfft_window_values",
     "zfft_plan_tune", "zfft_plan_timing", "zfft_plan_timings", "zfft_plan_timing_names",
     "zfft_plan_path", "zfft_plan_welch", "zfft_last_error",
+    "zfft_plan_config", "zfft_ring_create", "zfft_ring_destroy", "zfft_ring_add",
+    "zfft_ring_state", "zfft_ring_take", "zfft_ring_process",
     "zfft_colormap_lut", "zfft_waterfall_colormap", "zfft_waterfall_levels",
     "zfft_waterfall_get_levels", "zfft_waterfall_autolevel", "zfft_waterfall_render",
     "zfft_waterfall_render_device",
@@ -122,6 +124,15 @@ def load(path: str = ""):
         "zfft_plan_path": (ctypes.c_int, [P, I32]),
         "zfft_plan_welch": (ctypes.c_int, [P, I32]),
         "zfft_last_error": (ctypes.c_char_p, []),
+        "zfft_plan_config": (ctypes.c_int, [P, cfgp]),
+        "zfft_ring_create": (ctypes.c_int, [I64, I32, ctypes.POINTER(P)]),
+        "zfft_ring_destroy": (ctypes.c_int, [P]),
+        "zfft_ring_add": (ctypes.c_int, [P, P, I64]),
+        "zfft_ring_state": (ctypes.c_int, [P, ctypes.POINTER(I64), ctypes.POINTER(I64),
+                                            ctypes.POINTER(I64)]),
+        "zfft_ring_take": (ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(I64),
+                                           ctypes.POINTER(I64)]),
+        "zfft_ring_process": (ctypes.c_int, [P, P, P, ctypes.POINTER(I32)]),
         "zfft_colormap_lut": (ctypes.c_int, [ctypes.c_char_p, P]),
         "zfft_waterfall_colormap": (ctypes.c_int, [P, ctypes.c_char_p]),
         "zfft_waterfall_levels": (ctypes.c_int, [P, D, D]),

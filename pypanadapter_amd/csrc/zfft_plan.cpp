@@ -976,6 +976,12 @@ int zfft_plan_destroy(zfft_plan *p) {
   return ZFFT_OK;
 }
 
+int zfft_plan_config(const zfft_plan *p, zfft_config *out) {
+  if (!p || !out) return fail(ZFFT_EINVAL, "null argument");
+  *out = p->cfg;
+  return ZFFT_OK;
+}
+
 int zfft_plan_tune(zfft_plan *p, int32_t block, int32_t warm) {
   if (!p || block < 0 || warm < 0) return fail(ZFFT_EINVAL, "bad tune arguments");
   if (block && (block < 64 || block > (1 << 20)))

@@ -236,6 +236,82 @@ class ZoomFFT:
         self.scroll = int(scroll)
 
 
+_IN_DTYPES = {"complex64": (0, np.complex64, 1), "complex32": (1, np.float16, 2),
+              "cu8": (2, np.uint8, 2)}
+
+
+class IQRing:
+    """Host IQ accumulation ring: pypanadapter_thread.py's `Data`
+    (T:1400-1483) in pinned host memory, between the reader thread (`add`) and the PSD
+    worker (`take` / `process`).  See include/zfft.h zfft_ring_* for the semantics."""
+
+    def __init__(self, chunk_size: int = 8196 * 2, in_dtype: str = "complex64"):
+        self.lib = _lib.load()
+        if in_dtype not in _IN_DTYPES:
+            raise ValueError(f"in_dtype must be one of {sorted(_IN_DTYPES)}")
+        self.in_dtype = in_dtype
+        code, self._np, self._per = _IN_DTYPES[in_dtype]
+        self._ring = ctypes.c_void_p()
+        check(self.lib.zfft_ring_create(int(chunk_size), code, ctypes.byref(self._ring)),
+              "zfft_ring_create")
+        self.chunk_size = int(chunk_size)
+        self.max_size = 16 * self.chunk_size
+
+    def close(self):
+        if self._ring:
+            self.lib.zfft_ring_destroy(self._ring)
+            self._ring = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _raw(self, chunk) -> tuple:
+        a = np.ascontiguousarray(chunk)
+        if self.in_dtype == "complex64":
+            a = np.ascontiguousarray(a, dtype=np.complex64)
+            return a, a.shape[0]
+        a = np.ascontiguousarray(a, dtype=self._np).reshape(-1)
+        if a.size % 2:
+            raise ValueError("interleaved I,Q input needs an even number of values")
+        return a, a.size // 2
+
+    def add(self, chunk) -> None:
+        """Data.add (T:1433-1457) without the pacing sleep."""
+        a, n = self._raw(chunk)
+        check(self.lib.zfft_ring_add(self._ring, a.ctypes.data_as(ctypes.c_void_p), n),
+              "zfft_ring_add")
+
+    def state(self):
+        """(size, real_size, total_size) as Data holds them."""
+        v = [ctypes.c_int64() for _ in range(3)]
+        check(self.lib.zfft_ring_state(self._ring, *(ctypes.byref(x) for x in v)), "zfft_ring_state")
+        return tuple(x.value for x in v)
+
+    def take(self):
+        """get_data_start / data[:real_size] / get_data_end (T:1516-1520): the frame (a view
+        of the drained buffer, valid until the next take) and total_size."""
+        p, n, tot = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.zfft_ring_take(self._ring, ctypes.byref(p), ctypes.byref(n),
+                                      ctypes.byref(tot)), "zfft_ring_take")
+        count = n.value * self._per
+        if count == 0:
+            return np.empty(0, dtype=self._np), tot.value
+        buf = (ctypes.c_char * (count * np.dtype(self._np).itemsize)).from_address(p.value)
+        return np.frombuffer(buf, dtype=self._np, count=count), tot.value
+
+    def process(self, plan: "ZoomFFT"):
+        """PSD.update (T:1513-1548): the next row from the drained frame, or None when the
+        frame is shorter than fft_size (T:1522-1523)."""
+        row = np.empty(plan.n_win, dtype=np.float32)
+        produced = ctypes.c_int32()
+        check(self.lib.zfft_ring_process(self._ring, plan._plan, row.ctypes.data_as(ctypes.c_void_p),
+                                         ctypes.byref(produced)), "zfft_ring_process")
+        return row if produced.value else None
+
+
 def colormap_lut(name: str) -> np.ndarray:
     """The 256 x 4 RGBA lookup table of a Waterfall colormap (host-side, no GPU needed)."""
     lib = _lib.load()

@@ -172,3 +172,64 @@ class Waterfall:
     def render(self) -> np.ndarray:
         """RGBA uint8 (H, W, 4) in img_array's row order."""
         return self._need_plan().waterfall_render()
+
+
+class Data:
+    """pypanadapter_thread.py's `Data` (T:1400-1483) on the pinned double-buffered IQRing
+    (SURVEY §8f-1), same calls: the reader thread's `add(chunk)` (T:2191) and the PSD
+    worker's `get_data_start(); size = real_size; chunk = data[:size]; get_data_end()`
+    (T:1516-1520).  `get_data_start` drains the ring, so `data[:real_size]` stays intact
+    while the reader keeps adding (the reference hands out a view it keeps overwriting).
+    `in_dtype="cu8"` takes the RTL-SDR's raw interleaved uint8 I,Q bytes.  The NewtRap
+    pacing (`delay_time`) is out of scope; `target` is kept as a plain attribute."""
+
+    def __init__(self, chunk_size: int = 8196 * 2, in_dtype: str = "complex64"):
+        self.chunk_size = int(chunk_size)
+        self.max_size = self.chunk_size * 16
+        self.target_size = self.max_size * .9
+        self.in_dtype = in_dtype
+        self._ring = None
+        self.data = None
+        self.real_size = 0
+        self.total_size = 0
+
+    def new_complex(self):
+        from .engine import IQRing
+        if self._ring is not None:
+            self._ring.close()
+        self._ring = IQRing(self.chunk_size, self.in_dtype)
+        self.real = False
+        self.data, self.real_size, self.total_size = None, 0, 0
+        return self
+
+    def new_real(self):
+        raise NotImplementedError("real (AudioPan) input is SURVEY §8f-4, not built yet")
+
+    def add(self, chunk):
+        self._ring.add(chunk)
+
+    def get_data_start(self):
+        frame, total = self._ring.take()
+        self.data = frame
+        self.real_size = len(frame) if self.in_dtype == "complex64" else len(frame) // 2
+        self.total_size = total
+
+    def get_data_end(self):
+        pass  # the counts were reset by the drain in get_data_start
+
+    def process(self, plan):
+        """get_data_start + PSD.update's DSP in one call (zfft_ring_process)."""
+        return self._ring.process(plan)
+
+    @property
+    def target(self):
+        return self.target_size
+
+    @target.setter
+    def target(self, t):
+        if t <= self.max_size:
+            self.target_size = t
+
+    @property
+    def maxsize(self):
+        return self.max_size
