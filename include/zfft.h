@@ -78,7 +78,8 @@ typedef struct zfft_config {
   int32_t in_dtype;        /* 0 = complex64 (interleaved f32, 8 B/sample); 1 = complex32
                               (interleaved f16, 4 B/sample, BASELINE cfg5); 2 = RTL-SDR
                               interleaved uint8 I,Q (2 B/sample), value b/127.5 - 1 as
-                              pyrtlsdr's packed_bytes_to_iq                  */
+                              pyrtlsdr's packed_bytes_to_iq; 3 = real f32
+                              (4 B/sample: AudioPan's paFloat32 stream, S:712-713, §8f-4)  */
   int32_t device;          /* HIP device ordinal                                            */
   int32_t flip_input;      /* 1 = reverse each frame on load: the np.flip the RTL-SDR
                               sources apply (S:541-543, 459-460), fused into stage 0       */
@@ -92,6 +93,10 @@ typedef struct zfft_plan zfft_plan;
 int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_plan **out);
 int zfft_plan_destroy(zfft_plan *plan);
 int zfft_plan_config(const zfft_plan *plan, zfft_config *out);  /* the configuration in use */
+/* Valid floats per row (rows keep the stride n_win): n_win, except for real input
+ * (in_dtype 3) at zoom 1, where the reference's welch is one-sided and its
+ * fftshift(P)[N/2 - W/2 : N/2 + W/2] slice of the N/2+1 bins is shorter. */
+int zfft_plan_row_length(const zfft_plan *plan);
 
 /* Host-buffer path: n_frames frames of n_samples IQ each (frame-major), rows_out holds
  * n_frames*n_win floats.  Synchronous.  PCIe-inclusive. */

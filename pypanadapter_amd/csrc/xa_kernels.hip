@@ -106,10 +106,12 @@ template <int DT> struct Raw;
 template <> struct Raw<kInC64> { typedef v2f T; };
 template <> struct Raw<kInC32H> { typedef h2 T; };
 template <> struct Raw<kInCU8> { typedef u8x2 T; };
+template <> struct Raw<kInF32R> { typedef float T; };
 template <int DT>
 __device__ __forceinline__ v2f cvt_raw(typename Raw<DT>::T r) {  // as load_in_t (zfft_device.h)
   if constexpr (DT == kInC64) return r;
   else if constexpr (DT == kInC32H) return v2f{(float)r.x, (float)r.y};
+  else if constexpr (DT == kInF32R) return v2f{r, 0.f};
   else return v2f{((float)r.x - 127.5f) * (1.f / 127.5f), ((float)r.y - 127.5f) * (1.f / 127.5f)};
 }
 
@@ -862,6 +864,9 @@ hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix, 
   } else if (in.dtype == kInC32H) {
     if (in.flip) xa_launch<true, kInC32H, 1>(in, n, lo, out, frames, tab, st);
     else xa_launch<true, kInC32H, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInF32R) {
+    if (in.flip) xa_launch<true, kInF32R, 1>(in, n, lo, out, frames, tab, st);
+    else xa_launch<true, kInF32R, 0>(in, n, lo, out, frames, tab, st);
   } else {
     if (in.flip) xa_launch<true, kInCU8, 1>(in, n, lo, out, frames, tab, st);
     else xa_launch<true, kInCU8, 0>(in, n, lo, out, frames, tab, st);

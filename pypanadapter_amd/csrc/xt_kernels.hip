@@ -386,6 +386,9 @@ hipError_t launch_xt_stage(const InDesc &in, int n, const float2 *lo, bool mix, 
   } else if (in.dtype == kInC32H) {
     if (in.flip) xt_launch<true, kInC32H, 1>(in, n, lo, out, frames, tab, st);
     else xt_launch<true, kInC32H, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInF32R) {
+    if (in.flip) xt_launch<true, kInF32R, 1>(in, n, lo, out, frames, tab, st);
+    else xt_launch<true, kInF32R, 0>(in, n, lo, out, frames, tab, st);
   } else {
     if (in.flip) xt_launch<true, kInCU8, 1>(in, n, lo, out, frames, tab, st);
     else xt_launch<true, kInCU8, 0>(in, n, lo, out, frames, tab, st);

@@ -38,6 +38,8 @@ __device__ __forceinline__ v2f load_in_t(const InDesc &d, int64_t f, int64_t i) 
   } else if constexpr (DT == kInC32H) {
     const h2 h = ((const h2 *)d.p)[k];
     return v2f{(float)h.x, (float)h.y};
+  } else if constexpr (DT == kInF32R) {
+    return v2f{((const float *)d.p)[k], 0.f};
   } else {
     const u8x2 b = ((const u8x2 *)d.p)[k];
     return v2f{((float)b.x - 127.5f) * (1.f / 127.5f), ((float)b.y - 127.5f) * (1.f / 127.5f)};
@@ -47,6 +49,7 @@ __device__ __forceinline__ v2f load_in_t(const InDesc &d, int64_t f, int64_t i) 
 __device__ __forceinline__ v2f load_in(const InDesc &d, int64_t f, int64_t i) {
   if (d.dtype == kInC64) return load_in_t<kInC64>(d, f, i);
   if (d.dtype == kInC32H) return load_in_t<kInC32H>(d, f, i);
+  if (d.dtype == kInF32R) return load_in_t<kInF32R>(d, f, i);
   return load_in_t<kInCU8>(d, f, i);
 }
 

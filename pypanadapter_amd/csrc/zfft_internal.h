@@ -26,15 +26,16 @@ Sos32 sos32();
 // The caller's frames (the `chunk` of S:2102 / T:1516): sample i of frame f is element
 // f * stride + (flip ? len - 1 - i : i) of p, in one of the zfft_config in_dtype formats:
 //   0 complex64 (interleaved f32), 1 complex32 (interleaved f16, BASELINE cfg5),
-//   2 RTL-SDR interleaved uint8 I,Q, value b/127.5 - 1 (pyrtlsdr packed_bytes_to_iq).
+//   2 RTL-SDR interleaved uint8 I,Q, value b/127.5 - 1 (pyrtlsdr packed_bytes_to_iq),
+//   3 real float32 (AudioPan's pyaudio paFloat32 stream, S:712-713): I = x, Q = 0.
 // flip fuses the sources' np.flip (S:541-543, 459-460) into the stage-0 loads.
-enum InDtype { kInC64 = 0, kInC32H = 1, kInCU8 = 2 };
+enum InDtype { kInC64 = 0, kInC32H = 1, kInCU8 = 2, kInF32R = 3 };
 struct InDesc {
   const void *p;
   int64_t stride, len;
   int dtype, flip;
 };
-inline size_t in_elem_bytes(int dtype) { return dtype == kInC64 ? 8 : dtype == kInC32H ? 4 : 2; }
+inline size_t in_elem_bytes(int dtype) { return dtype == kInC64 ? 8 : (dtype == kInC32H || dtype == kInF32R) ? 4 : 2; }
 
 // --- kernels (zfft_kernels.hip); all enqueue on `st`, return hipError_t of the launch ---
 // Intermediates use the frame-group-interleaved (FGI) layout: element (f, j) of a
@@ -140,6 +141,10 @@ struct WelchGeom {
   int n_win;
   int nperseg, step, nseg;
   float scale;  // 1 / (fs * sum(w^2) * nseg)
+  // one-sided (real input at zoom 1, scipy's rfft branch): bins 0..N/2,
+  // doubled except 0 and N/2, then the reference's fftshift of those N/2+1 bins and its
+  // [N/2 - W/2, N/2 + W/2) slice -- row_len = that slice's length, from row_a
+  int onesided = 0, row_a = 0, row_len = 0;
 };
 
 hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, const float2 *tw,

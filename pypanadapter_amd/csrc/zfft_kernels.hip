@@ -427,6 +427,22 @@ __device__ __forceinline__ v2f wave_sum(v2f v) {
   return v;
 }
 
+// Row slot of bin k (-1: cropped) and its one-sided factor.  Two-sided: fftshift + crop,
+// row[j] = P[(j - W/2) mod N].  One-sided (WelchGeom::onesided): position
+// (k + M/2) mod M of the fftshift of the M = N/2+1 bins, minus the slice start row_a.
+__device__ __forceinline__ int welch_slot(const WelchGeom &g, int k, float &mult) {
+  mult = 1.f;
+  if (!g.onesided) {
+    const int j = (k + (g.n_win >> 1)) & (g.n_fft - 1);
+    return j < g.n_win ? j : -1;
+  }
+  const int h = g.n_fft >> 1, M = h + 1;
+  if (k > h) return -1;
+  if (k != 0 && k != h) mult = 2.f;
+  const int j = (k + M / 2) % M - g.row_a;
+  return (j >= 0 && j < g.row_len) ? j : -1;
+}
+
 // ---- in-register DFTs (forward, exp(-2 pi i k n / R)) ----
 __device__ __forceinline__ v2f mul_negi(v2f a) { return v2f{a.y, -a.x}; }  // -i * a
 
@@ -650,8 +666,9 @@ __global__ __launch_bounds__(MAXT, (MAXT == 256 ? WELCH_MINB : 1)) void welch_ro
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int k = N == R0 ? stockham_out_index<R0>(t, N, 1, i) : stockham_out_index<16>(t, N, lastNs, i);
-    const int j = (k + (g.n_win >> 1)) & (N - 1);  // fftshift + crop: row[j] = P[(j - W/2) mod N]
-    if (j < g.n_win) row[j] = 20.f * log10f(acc[i] * g.scale);
+    float mult;
+    const int j = welch_slot(g, k, mult);
+    if (j >= 0) row[j] = 20.f * log10f(acc[i] * g.scale * mult);
   }
 }
 
@@ -757,8 +774,9 @@ __global__ __launch_bounds__(MAXT) void welch_rows2_kernel(const v2f *__restrict
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int k = N == R0 ? stockham_out_index<R0>(t, N, 1, i) : stockham_out_index<16>(t, N, lastNs, i);
-    const int j = (k + (g.n_win >> 1)) & (N - 1);  // fftshift + crop: row[j] = P[(j - W/2) mod N]
-    if (j < g.n_win) row[j] = 20.f * log10f(acc[i] * g.scale);
+    float mult;
+    const int j = welch_slot(g, k, mult);
+    if (j >= 0) row[j] = 20.f * log10f(acc[i] * g.scale * mult);
   }
 }
 
@@ -997,8 +1015,9 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
   for (int i = 0; i < NACC; ++i) {
     const int q = PRUNE ? 16 * t + D::RL * (i >> 1) + ((i & 1) ? D::RL - 1 : 0) : 16 * t + i;
     const int k = dif_bin<N>(q);
-    const int j = (k + (g.n_win >> 1)) & (N - 1);  // fftshift + crop: row[j] = P[(j - W/2) mod N]
-    if (j < g.n_win) row[j] = 20.f * log10f(acc[i] * g.scale);
+    float mult;
+    const int j = welch_slot(g, k, mult);
+    if (j >= 0) row[j] = 20.f * log10f(acc[i] * g.scale * mult);
   }
 }
 
@@ -1007,7 +1026,7 @@ static hipError_t welch_dif_launch(const float2 *x, int64_t len, const float *wi
                                    const WelchGeom &g, float *rows, int frames, hipStream_t st) {
   using D = Dif<N>;
   const size_t lds = (size_t)D::FPB * D::SLOTS * sizeof(v2f);
-  const bool prune = g.n_win <= 2 * N / D::RL;
+  const bool prune = !g.onesided && g.n_win <= 2 * N / D::RL;
   const void *k = prune ? (const void *)welch_dif_kernel<N, true> : (const void *)welch_dif_kernel<N, false>;
   static bool attr_set[2] = {false, false};
   if (lds > 48 * 1024 && !attr_set[prune]) {
@@ -1125,8 +1144,9 @@ __global__ __launch_bounds__(256) void welch4_rows_kernel(const v2f *__restrict_
   for (int i = 0; i < 16; ++i) {
     const int k1 = N1 == R0 ? stockham_out_index<R0>(t, N1, 1, i) : stockham_out_index<16>(t, N1, R0, i);
     const int k = k2 + kN2 * k1;
-    const int j = (k + (g.n_win >> 1)) & (N - 1);  // row[j] = P[(j - W/2) mod N]
-    if (j < g.n_win) row[j] = 20.f * log10f(acc[i] * g.scale);
+    float mult;
+    const int j = welch_slot(g, k, mult);
+    if (j >= 0) row[j] = 20.f * log10f(acc[i] * g.scale * mult);
   }
 }
 
@@ -1248,6 +1268,8 @@ hipError_t launch_iir_forward_mix(const InDesc &in, int frames, const float2 *lo
     hipLaunchKernelGGL(iir_forward_mix_kernel<kInC64>, grid, block, 0, st, in, frames, l, y, g, sos32());
   else if (in.dtype == kInC32H)
     hipLaunchKernelGGL(iir_forward_mix_kernel<kInC32H>, grid, block, 0, st, in, frames, l, y, g, sos32());
+  else if (in.dtype == kInF32R)
+    hipLaunchKernelGGL(iir_forward_mix_kernel<kInF32R>, grid, block, 0, st, in, frames, l, y, g, sos32());
   else
     hipLaunchKernelGGL(iir_forward_mix_kernel<kInCU8>, grid, block, 0, st, in, frames, l, y, g, sos32());
   return hipGetLastError();
@@ -1302,6 +1324,8 @@ hipError_t launch_ingest(const InDesc &in, const float2 *lo, float2 *out, int fr
     hipLaunchKernelGGL(ingest_kernel<kInC64>, grid, block, 0, st, in, l, o, total);
   else if (in.dtype == kInC32H)
     hipLaunchKernelGGL(ingest_kernel<kInC32H>, grid, block, 0, st, in, l, o, total);
+  else if (in.dtype == kInF32R)
+    hipLaunchKernelGGL(ingest_kernel<kInF32R>, grid, block, 0, st, in, l, o, total);
   else
     hipLaunchKernelGGL(ingest_kernel<kInCU8>, grid, block, 0, st, in, l, o, total);
   return hipGetLastError();

@@ -6,6 +6,7 @@
 // window / twiddle tables, a grow-only workspace and the waterfall ring.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <cstring>
@@ -770,6 +771,18 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   return run_exact(p, in, p->lo.as<float2>(), frames, n, out, st);
 }
 
+// Real input at zoom 1 takes scipy.signal.welch's one-sided branch.
+bool onesided(const zfft_plan *p) { return p->cfg.in_dtype == kInF32R && p->K == 0; }
+
+// Valid entries per row: W, or in the one-sided case the length of the reference's slice
+// fftshift(P)[N/2 - W/2 : N/2 + W/2] of the N/2+1 one-sided bins.
+int row_length(const zfft_plan *p) {
+  const int N = p->cfg.n_fft, W = p->cfg.n_win;
+  if (!onesided(p)) return W;
+  const int a = N / 2 - W / 2, b = std::min(N / 2 + W / 2, N / 2 + 1);
+  return std::max(0, b - a);
+}
+
 InDesc input_of(const zfft_plan *p, const void *d_iq, int64_t L) {
   return InDesc{d_iq, L, L, p->cfg.in_dtype, p->cfg.flip_input};
 }
@@ -808,6 +821,11 @@ int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, fl
   w.nseg = (int)((Ld - nperseg) / w.step + 1);
   // density scaling 1/(fs*sum(w^2)) and the segment mean (csd average='mean')
   w.scale = (float)(1.0 / (p->cfg.fs * p->win_ss * (double)w.nseg));
+  if (onesided(p)) {
+    w.onesided = 1;
+    w.row_a = N / 2 - p->cfg.n_win / 2;
+    w.row_len = row_length(p);
+  }
   // auto: four-step above 8192 (cfg3, N = 16384: 1.86 ms against 2.20 for one workgroup
   // per frame, MI355X); it is the only form above kMaxLdsFft
   const bool four = p->welch == 2 || (p->welch == 0 && N > 8192);
@@ -890,8 +908,8 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
   if (!(c.fs > 0) || !std::isfinite(c.fs) || !std::isfinite(c.f_lo))
     return fail(ZFFT_EINVAL, "fs must be positive and finite, f_lo finite");
   if (c.scroll != 1 && c.scroll != -1) return fail(ZFFT_EINVAL, "scroll must be +1 or -1");
-  if (c.in_dtype < kInC64 || c.in_dtype > kInCU8)
-    return fail(ZFFT_EINVAL, "in_dtype must be 0 (complex64), 1 (complex32 f16) or 2 (RTL-SDR u8)");
+  if (c.in_dtype < kInC64 || c.in_dtype > kInF32R)
+    return fail(ZFFT_EINVAL, "in_dtype must be 0 (complex64), 1 (complex32 f16), 2 (RTL-SDR u8) or 3 (real f32)");
   if (c.flip_input != 0 && c.flip_input != 1) return fail(ZFFT_EINVAL, "flip_input must be 0 or 1");
   if (c.window_kind == ZFFT_WIN_ARRAY) {
     if (!window_or_null) return fail(ZFFT_EINVAL, "ZFFT_WIN_ARRAY needs a window array");
@@ -974,6 +992,11 @@ int zfft_plan_destroy(zfft_plan *p) {
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
   return ZFFT_OK;
+}
+
+int zfft_plan_row_length(const zfft_plan *p) {
+  if (!p) return fail(ZFFT_EINVAL, "null plan");
+  return row_length(p);
 }
 
 int zfft_plan_config(const zfft_plan *p, zfft_config *out) {

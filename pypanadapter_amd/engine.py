@@ -38,7 +38,8 @@ def _window_spec(window):
 
 
 # in_dtype name -> (zfft_config.in_dtype, numpy element type of the host array)
-IN_DTYPES = {"complex64": (0, np.complex64), "complex32": (1, np.float16), "cu8": (2, np.uint8)}
+IN_DTYPES = {"complex64": (0, np.complex64), "complex32": (1, np.float16), "cu8": (2, np.uint8),
+             "f32": (3, np.float32)}
 
 
 class ZoomFFT:
@@ -48,7 +49,8 @@ class ZoomFFT:
                  window="hamming", f_lo: float = 1.0, scroll: int = 1, device: int = 0,
                  in_dtype: str = "complex64", flip: bool = False):
         """in_dtype: "complex64" (complex ndarray), "complex32" (float16 interleaved I,Q,
-        shape (..., 2L)) or "cu8" (RTL-SDR uint8 interleaved I,Q, value b/127.5 - 1).
+        shape (..., 2L)), "cu8" (RTL-SDR uint8 interleaved I,Q, value b/127.5 - 1) or "f32"
+        (real samples, AudioPan; at zoom 1 the rows are one-sided and `row_length` long).
         flip: reverse every frame on load (the sources' np.flip, S:541-543)."""
         self.lib = _lib.load()
         if in_dtype not in IN_DTYPES:
@@ -128,13 +130,25 @@ class ZoomFFT:
         if self.in_dtype == "complex64":
             if x.dtype != dt:
                 x = x.astype(dt)
+        elif self.in_dtype == "f32":
+            if np.iscomplexobj(x):
+                raise ValueError("f32 input must be real")
+            x = x.astype(dt, copy=False)
         elif x.dtype != dt or x.shape[-1] % 2:
             raise ValueError(f"{self.in_dtype} input must be {np.dtype(dt).name} with "
                              "interleaved I,Q on the last axis")
         return np.ascontiguousarray(x)
 
     def _samples(self, x) -> int:
-        return x.shape[-1] if self.in_dtype == "complex64" else x.shape[-1] // 2
+        return x.shape[-1] if self.in_dtype in ("complex64", "f32") else x.shape[-1] // 2
+
+    @property
+    def row_length(self) -> int:
+        """Valid floats per row: n_win, or the one-sided slice for real input at zoom 1."""
+        n = self.lib.zfft_plan_row_length(self._plan)
+        if n < 0:
+            check(n, "zfft_plan_row_length")
+        return n
 
     def rows(self, frames) -> np.ndarray:
         """(F, L) or (L,) complex IQ -> (F, W) or (W,) float32 dB rows."""
@@ -145,6 +159,9 @@ class ZoomFFT:
         out = np.empty((F, self.n_win), dtype=np.float32)
         check(self.lib.zfft_process(self._plan, x2.ctypes.data_as(ctypes.c_void_p), L, F,
                                     out.ctypes.data_as(ctypes.c_void_p)), "zfft_process")
+        n = self.row_length
+        if n != self.n_win:  # one-sided rows (real input at zoom 1)
+            out = np.ascontiguousarray(out[:, :n])
         return out[0] if single else out
 
     def process_device(self, d_iq_ptr: int, n_samples: int, n_frames: int, d_rows_ptr: int,
@@ -237,7 +254,7 @@ class ZoomFFT:
 
 
 _IN_DTYPES = {"complex64": (0, np.complex64, 1), "complex32": (1, np.float16, 2),
-              "cu8": (2, np.uint8, 2)}
+              "cu8": (2, np.uint8, 2), "f32": (3, np.float32, 1)}
 
 
 class IQRing:
@@ -270,8 +287,8 @@ class IQRing:
 
     def _raw(self, chunk) -> tuple:
         a = np.ascontiguousarray(chunk)
-        if self.in_dtype == "complex64":
-            a = np.ascontiguousarray(a, dtype=np.complex64)
+        if self.in_dtype in ("complex64", "f32"):
+            a = np.ascontiguousarray(a, dtype=self._np).reshape(-1)
             return a, a.shape[0]
         a = np.ascontiguousarray(a, dtype=self._np).reshape(-1)
         if a.size % 2:
@@ -309,7 +326,7 @@ class IQRing:
         produced = ctypes.c_int32()
         check(self.lib.zfft_ring_process(self._ring, plan._plan, row.ctypes.data_as(ctypes.c_void_p),
                                          ctypes.byref(produced)), "zfft_ring_process")
-        return row if produced.value else None
+        return row[:plan.row_length] if produced.value else None
 
 
 def colormap_lut(name: str) -> np.ndarray:

@@ -40,13 +40,14 @@ class PlanCache:
         self._key = None
         self.plan: ZoomFFT | None = None
 
-    def get(self, fs, n_fft, zoom, n_win, window="hamming", f_lo=1.0) -> ZoomFFT:
-        key = (float(fs), int(n_fft), int(zoom), int(n_win), _key(window), float(f_lo))
+    def get(self, fs, n_fft, zoom, n_win, window="hamming", f_lo=1.0,
+            in_dtype="complex64") -> ZoomFFT:
+        key = (float(fs), int(n_fft), int(zoom), int(n_win), _key(window), float(f_lo), in_dtype)
         if key != self._key:
             if self.plan is not None:
                 self.plan.close()
             self.plan = ZoomFFT(n_fft, zoom, fs, n_win=n_win, window=window, f_lo=f_lo,
-                                device=self.device)
+                                device=self.device, in_dtype=in_dtype)
             self._key = key
         return self.plan
 
@@ -71,10 +72,14 @@ def psd_row(chunk, fs: float, fft_size: int, fft_ratio: int, n_win: int | None =
     """The row ApplicationDisplay.update hands to waterfall.image_update (S:2102-2119).
 
     Returns a fresh, writable float64 array (the reference's dtype), length n_win
-    (default N / zoom, i.e. N_WIN after fft_change, S:1757).
+    (default N / zoom, i.e. N_WIN after fft_change, S:1757).  A real chunk (AudioPan,
+    S:712-713) runs as real input: mixed to complex by the LO when zooming, and through
+    welch's one-sided branch at zoom 1, whose row is the reference's shorter slice.
     """
     n_win = int(fft_size) // int(fft_ratio) if n_win is None else int(n_win)
-    plan = _cache(device).get(fs, fft_size, fft_ratio, n_win, window, f_lo)
+    real = not np.iscomplexobj(chunk)
+    plan = _cache(device).get(fs, fft_size, fft_ratio, n_win, window, f_lo,
+                              "f32" if real else "complex64")
     return plan.rows(chunk).astype(np.float64)
 
 
@@ -211,7 +216,7 @@ class Data:
     def get_data_start(self):
         frame, total = self._ring.take()
         self.data = frame
-        self.real_size = len(frame) if self.in_dtype == "complex64" else len(frame) // 2
+        self.real_size = len(frame) if self.in_dtype in ("complex64", "f32") else len(frame) // 2
         self.total_size = total
 
     def get_data_end(self):

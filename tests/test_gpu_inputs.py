@@ -97,3 +97,54 @@ def test_input_format_rejects_wrong_arrays():
             plan.rows(np.zeros(4097, np.uint8))
     with pytest.raises(ValueError):
         ZoomFFT(1024, 4, 2.4e6, in_dtype="complex128")
+
+
+def _audio(L, fs, seed):
+    """Real float32 'audio': two tones over white noise (AudioPan's paFloat32 stream)."""
+    rng = np.random.default_rng(seed)
+    n = np.arange(L)
+    x = 0.1 * rng.standard_normal(L) + np.sin(2 * np.pi * 0.123 * n) + 0.01 * np.cos(2 * np.pi * 0.31 * n)
+    return x.astype(np.float32)
+
+
+REAL_CASES = [(1024, 1, 1024, 12 * 1024), (1024, 1, 512, 12 * 1024), (2048, 1, 256, 9000),
+              (4096, 1, 4096, 40000), (256, 1, 256, 300), (1024, 4, 256, 64 * 1024),
+              (2048, 2, 1024, 30000)]
+
+
+@pytest.mark.parametrize("N,z,W,L", REAL_CASES, ids=[f"N{c[0]}_z{c[1]}_W{c[2]}_L{c[3]}" for c in REAL_CASES])
+def test_real_input_rows_vs_reference(N, z, W, L):
+    """Real input (AudioPan S:663-721): at zoom 1 scipy's welch is one-sided
+    (rfft bins 0..N/2, doubled but for 0 and N/2) and the reference's fftshift/crop slice
+    of those N/2+1 bins is shorter than W; when zooming the LO mix makes it complex.  The
+    oracle is the reference's own scipy calls on the same float32 samples.  Every schedule
+    and every Welch form."""
+    from oracle import scipy_path
+    from pypanadapter_amd import ZoomFFT
+    fs = 44100.0
+    x = np.stack([_audio(L, fs, 40 + f) for f in range(2)])
+    refs = [scipy_path.psd_row(x[f], fs, N, z, W) for f in range(2)]
+    assert (len(refs[0]) < W) == (z == 1)
+    paths = [0, 1, 3, 4] if z > 1 else [0]
+    welchs = [0, 1, 2] if (z == 1 and N >= 4096) else [0, 1]
+    for path in paths:
+        for welch in welchs:
+            with ZoomFFT(N, z, fs, n_win=W, in_dtype="f32") as plan:
+                plan.set_path(path)
+                plan.set_welch(welch)
+                rows = plan.rows(x)
+                assert plan.row_length == len(refs[0])
+            for f in range(2):
+                assert_row_close(rows[f], refs[f], f"real path={path} welch={welch} frame {f}")
+
+
+def test_real_chunk_through_the_facade():
+    """psd_row with a real chunk (what S:2102-2119 gets from AudioPan) takes the real path."""
+    from oracle import scipy_path
+    from pypanadapter_amd import psd_row
+    x = _audio(20000, 44100.0, 7)
+    for z, W in ((1, 1024), (2, 1024)):
+        row = psd_row(x, 44100.0, 2048, z, W)
+        ref = scipy_path.psd_row(x, 44100.0, 2048, z, W)
+        assert row.shape == ref.shape
+        assert_row_close(row, ref, f"facade z={z}")
