@@ -408,17 +408,31 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         for (int k = 0; k < kXaK / 2; ++k) hw[k] = v4f{h[2 * k].x, h[2 * k].y, h[2 * k + 1].x, h[2 * k + 1].y};
       }
       __builtin_amdgcn_wave_barrier();
-      // output idx = 64 c + ln (c in this half) sits at row idx/16 - 32 hf, column ln % 16
+      // output idx = 64 c + ln (c in this half) sits at row idx/16 - 32 hf, column ln % 16;
+      // all the half's chunks are read first (one LDS round trip), then stored: an interior
+      // tile (wave-uniform `inside`) stores without per-chunk tests
       const LP hr = buf + (ln >> 4) * kHeldRow + (ln & 15);
+      v2f vc[kChunks / 2];
+#pragma unroll
+      for (int cc = 0; cc < kChunks / 2; ++cc) vc[cc] = hr[cc * 4 * kHeldRow];
+      if (inside) {
+#pragma unroll
+        for (int cc = 0; cc < kChunks / 2; ++cc) {
+          const int c = hf * (kChunks / 2) + cc;
+          if (c < kChunks - kLagChunks && !XA_DIAG_NOSTORE) od[64 * c] = vc[cc];
+        }
+      } else {
+#pragma unroll
+        for (int cc = 0; cc < kChunks / 2; ++cc) {
+          const int c = hf * (kChunks / 2) + cc;
+          if (c < kChunks - kLagChunks && m0 + 64 * c >= 0 && m0 + 64 * c < n_out && !XA_DIAG_NOSTORE)
+            od[64 * c] = vc[cc];
+        }
+      }
 #pragma unroll
       for (int cc = 0; cc < kChunks / 2; ++cc) {
         const int c = hf * (kChunks / 2) + cc;
-        const v2f v = hr[cc * 4 * kHeldRow];
-        if (c >= kChunks - kLagChunks) {
-          held[c - (kChunks - kLagChunks)] = v;
-        } else if (inside || (m0 + 64 * c >= 0 && m0 + 64 * c < n_out)) {
-          if (!XA_DIAG_NOSTORE) od[64 * c] = v;
-        }
+        if (c >= kChunks - kLagChunks) held[c - (kChunks - kLagChunks)] = vc[cc];
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -439,8 +453,20 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
         v = vfma(splat(l1.z), q->r[6], v);
         v = vfma(splat(l1.w), q->r[7], v);
       }
-      const int m = m0 + 64 * c;
-      if (m >= 0 && m < n_out && !XA_DIAG_NOSTORE) o[m] = v;
+      held[c] = v;
+    }
+    // wave-uniform: every held output of the tile inside the frame -> unconditional stores
+    const bool inside = m_of(tile, (kChunks - kLagChunks) * 64) >= 0 && m_of(tile, kChunks * 64) <= n_out;
+    if (inside) {
+#pragma unroll
+      for (int c = 0; c < kLagChunks; ++c)
+        if (!XA_DIAG_NOSTORE) o[m0 + 64 * c] = held[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < kLagChunks; ++c) {
+        const int m = m0 + 64 * c;
+        if (m >= 0 && m < n_out && !XA_DIAG_NOSTORE) o[m] = held[c];
+      }
     }
   };
 
