@@ -27,7 +27,8 @@ def needs_build() -> bool:
 def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH,
           defines: tuple = ()) -> str:
     """hipcc all sources into `out`; `defines` ("NAME=VALUE", ...) select kernel build knobs
-    (A/B variants written elsewhere than the shipped LIB_PATH)."""
+    (A/B variants written elsewhere than the shipped LIB_PATH); an entry starting with "-" is
+    passed to hipcc as it is (e.g. "-mllvm", "-amdgpu-sched-strategy=max-ilp")."""
     if not force and not defines and out == LIB_PATH and not needs_build():
         return LIB_PATH
     os.makedirs(os.path.dirname(out), exist_ok=True)
@@ -35,7 +36,7 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH,
     tmp = out + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
-    cmd += [f"-D{d}" for d in defines]
+    cmd += [d if d.startswith("-") else f"-D{d}" for d in defines]
     cmd += [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp]
     if verbose:
         print(" ".join(cmd))

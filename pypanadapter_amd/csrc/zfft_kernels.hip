@@ -1164,36 +1164,43 @@ __device__ __forceinline__ int pmod(int64_t a, int m) {
   return r < 0 ? r + m : r;
 }
 
-// Applies pushes [max(0,count-H), count) in order (earlier ones are fully overwritten:
-// with a constant scroll every slot and every stamp is rewritten within H pushes).
-__global__ __launch_bounds__(1024) void waterfall_push_kernel(float *ring, int H, int W,
-                                                              const float *__restrict__ rows,
-                                                              int64_t row_stride, int count,
-                                                              int64_t off0, int scroll) {
-  const int T = blockDim.x, tid = threadIdx.x;
-  const int first = count > H ? count - H : 0;
-  int o = pmod(off0 + (int64_t)first * scroll, H);
+// Applies pushes [first, count), first = max(0, count - H), as the reference's sequence of
+// image_update calls would (earlier pushes are fully overwritten: every slot and stamp is
+// rewritten within H pushes), in parallel for scroll = +-1 (the reference's two scroll
+// directions, S:2074-2077; the plan admits no other), in two launches.  Push r (first <= r < count) writes slot
+// s_r = (H - 1 + off0 + r scroll) mod H -- distinct slots, since count - first <= H -- so
+// every row lands at once (waterfall_rows_kernel).  Its tick stamps then hit slots
+// q = (y + off0 + (r + 1) scroll) mod H; a stamp survives iff no later push rewrote q, i.e.
+// q has no writer in the batch or its writer r' <= r (waterfall_stamps_kernel).
+__global__ __launch_bounds__(256) void waterfall_rows_kernel(float *ring, int H, int W,
+                                                             const float *__restrict__ rows,
+                                                             int64_t row_stride, int first,
+                                                             int64_t off0, int scroll) {
+  const int xcol = blockIdx.x * 256 + threadIdx.x;
+  if (xcol >= W) return;
+  const int r = first + (int)blockIdx.y;
+  const int slot = pmod(H - 1 + off0 + (int64_t)r * scroll, H);
+  float v = rows[(int64_t)r * row_stride + xcol];
+  if (xcol == 0 || xcol == (W >> 1) || xcol == W - 1) v = 0.f;  // grid, S:1646-1648
+  ring[(int64_t)slot * W + xcol] = v;
+}
+
+__global__ __launch_bounds__(256) void waterfall_stamps_kernel(float *ring, int H, int W, int first,
+                                                               int count, int64_t off0, int scroll) {
   const int tick = W / 10;
   const int nt = (W - 1 + tick - 1) / tick;  // len(range(0, W-1, W//10))
   const int nrows = scroll > 0 ? 10 : 8;     // img[5:15] or img[-10:-2]
-  for (int r = first; r < count; ++r) {
-    const float *__restrict__ src = rows + (int64_t)r * row_stride;
-    const int slot = pmod(H - 1 + o, H);     // img[-1:] = psd
-    for (int xcol = tid; xcol < W; xcol += T) {
-      float v = src[xcol];
-      if (xcol == 0 || xcol == (W >> 1) || xcol == W - 1) v = 0.f;  // grid, S:1646-1648
-      ring[(int64_t)slot * W + xcol] = v;
-    }
-    o = pmod(o + scroll, H);
-    __syncthreads();
-    for (int idx = tid; idx < nt * nrows; idx += T) {  // tick stamps, S:1655-1662
-      const int i = idx % nt, yy = idx / nt;
-      if (i == 5 || i == 10) continue;
-      const int yrow = scroll > 0 ? 5 + yy : H - 10 + yy;
-      ring[(int64_t)pmod(yrow + o, H) * W + i * tick] = 0.f;
-    }
-    __syncthreads();
-  }
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)(count - first) * nrows * nt) return;
+  const int i = (int)(idx % nt), yy = (int)((idx / nt) % nrows);
+  const int r = first + (int)(idx / ((int64_t)nt * nrows));
+  if (i == 5 || i == 10) return;  // S:1655-1662
+  const int yrow = scroll > 0 ? 5 + yy : H - 10 + yy;
+  const int q = pmod(yrow + off0 + (int64_t)(r + 1) * scroll, H);
+  // the push writing slot q: (H - 1 + off0 + w scroll) = q (mod H), w in [first, first + H)
+  const int w = first + pmod((int64_t)scroll * (q + 1 - off0) - first, H);
+  if (w < count && w > r) return;  // rewritten by a later push
+  ring[(int64_t)q * W + i * tick] = 0.f;
 }
 
 // Waterfall rendering: pyqtgraph makeARGB of the ring image, pixel order as
@@ -1452,10 +1459,17 @@ hipError_t launch_waterfall_init(float *ring, int H, int W, hipStream_t st) {
 hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,
                                  int64_t row_stride, int count, int64_t off0, int scroll,
                                  hipStream_t st) {
-  const int T = W >= 1024 ? 1024 : (W >= 256 ? 256 : 64);
-  hipLaunchKernelGGL(waterfall_push_kernel, dim3(1), dim3(T), 0, st, ring, H, W, rows, row_stride,
-                     count, off0, scroll);
-  return hipGetLastError();
+  if (count <= 0) return hipSuccess;
+  if (scroll == 1 || scroll == -1) {  // ring rows, then the stamps that survive
+    const int first = count > H ? count - H : 0;
+    hipLaunchKernelGGL(waterfall_rows_kernel, dim3((unsigned)((W + 255) / 256), (unsigned)(count - first)),
+                       dim3(256), 0, st, ring, H, W, rows, row_stride, first, off0, scroll);
+    const int tick = W / 10, nt = (W - 1 + tick - 1) / tick, nrows = scroll > 0 ? 10 : 8;
+    hipLaunchKernelGGL(waterfall_stamps_kernel, dim3(nblocks((int64_t)(count - first) * nrows * nt, 256)),
+                       dim3(256), 0, st, ring, H, W, first, count, off0, scroll);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;  // (zfft_plan validates scroll)
 }
 
 hipError_t launch_waterfall_read(const float *ring, int H, int W, int64_t off, float *img,

@@ -135,6 +135,34 @@ def test_waterfall_facade_stamps_row_in_place():
     assert w.img_array.dtype == np.float64
 
 
+@pytest.mark.parametrize("W", [64, 512])
+@pytest.mark.parametrize("scroll", [1, -1])
+def test_waterfall_batch_push_matches_sequence(W, scroll):
+    """zfft_waterfall_push_device of K rows at once (the parallel row + surviving-stamp
+    launches) equals K reference image_update calls in order, for K < H, K = H and K > H,
+    from a ring already offset by single pushes."""
+    import torch
+    from oracle.scipy_path import Waterfall as RefWaterfall
+    from pypanadapter_amd import ZoomFFT
+    H = W // 4
+    rng = np.random.default_rng(W + scroll)
+    with ZoomFFT(4096, 1, 2.4e6, n_win=W, scroll=scroll) as plan:
+        ref = RefWaterfall()
+        for k in range(3):
+            row = rng.uniform(-200, -100, W).astype(np.float32)
+            plan.waterfall_push(row)
+            ref.image_update(row.astype(np.float64), scroll)
+        for K in (5, H, H + 7):
+            rows = rng.uniform(-200, -100, (K, W)).astype(np.float32)
+            d = torch.from_numpy(rows).cuda()
+            plan.waterfall_push_device(d.data_ptr(), K, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            for r in rows:
+                ref.image_update(r.astype(np.float64), scroll)
+            np.testing.assert_array_equal(plan.waterfall_image(), ref.img_array.astype(np.float32),
+                                          err_msg=f"W={W} scroll={scroll} K={K}")
+
+
 def _frames(F, L, N, z, W, seed0=100, fs=2.4e6, f_lo=1.0):
     from pypanadapter_amd import synth
     return np.stack([synth.make_iq(L, fs, seed0 + f, n_fft=N, zoom=z, n_win=W, f_lo=f_lo)
