@@ -944,7 +944,18 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
     }
     const bool more = s + 1 < g.nseg;
     // (addresses from the loop-invariant thread id: computed once, outside the loop)
-    if (more) load_seg(pf, s + 1, (int)threadIdx.x % T);  // in flight during this segment's transform
+    if (more) {  // in flight during this segment's transform
+      if (2 * g.step == N) {
+        // 50 % overlap (scipy's default noverlap): segment s+1's values [0, 8) are this
+        // segment's raw [8, 16) -- only [8, PF) are loaded
+        const v2f *__restrict__ nseg = xf + (int64_t)(s + 1) * g.step;
+        const int tt = (int)threadIdx.x % T;
+#pragma unroll
+        for (int r = 0; r < PF; ++r) pf[r] = r < 8 ? v[r + 8] : nseg[tt + T * r];
+      } else {
+        load_seg(pf, s + 1, (int)threadIdx.x % T);
+      }
+    }
     {
       v2f sum = splat(0.f);
 #pragma unroll
