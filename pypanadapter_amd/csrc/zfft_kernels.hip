@@ -1111,12 +1111,23 @@ __global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict_
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = col[lp(t + r * 16)];
   stockham_pass<16>(v, t, kN2, 16, tws);
+  // output i is k2 = t + 16 i (stockham_out_index<16>(t, 256, 16, i)): its twiddle
+  // W_N^(n1 k2) = W_N^(n1 t) b^i with b = W_N^(16 n1), the powers of b formed from b, b^2,
+  // b^4, b^8 (at most three products deep) instead of 16 gathers from the length-N table
+  {
+    const v2f a = tw[n1 * t];
+    v2f bp[4];
+    bp[0] = tw[16 * n1];
+    bp[1] = cmul(bp[0], bp[0]);
+    bp[2] = cmul(bp[1], bp[1]);
+    bp[3] = cmul(bp[2], bp[2]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = cmul(v[i], a);
+    apply_powers(v, bp);
+  }
   v2f *__restrict__ zs = z + (int64_t)fs * N;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k2 = stockham_out_index<16>(t, kN2, 16, i);
-    zs[(int64_t)k2 * N1 + n1] = cmul(v[i], tw[n1 * k2]);
-  }
+  for (int i = 0; i < 16; ++i) zs[(int64_t)(t + 16 * i) * N1 + n1] = v[i];
 }
 
 template <int R0>
