@@ -516,6 +516,28 @@ __device__ __forceinline__ void dft<16>(v2f *v) {
   }
 }
 
+// v[r] *= b^r, r = 1..15, from bp = {b, b^2, b^4, b^8}: each power applied as soon as it
+// is formed (at most eight of them live)
+__device__ __forceinline__ void apply_powers(v2f *v, const v2f *bp) {
+  v[1] = cmul(v[1], bp[0]);
+  v[2] = cmul(v[2], bp[1]);
+  v[4] = cmul(v[4], bp[2]);
+  v[8] = cmul(v[8], bp[3]);
+  const v2f w3 = cmul(bp[0], bp[1]), w5 = cmul(bp[0], bp[2]), w6 = cmul(bp[1], bp[2]);
+  const v2f w7 = cmul(w3, bp[2]);
+  v[3] = cmul(v[3], w3);
+  v[5] = cmul(v[5], w5);
+  v[6] = cmul(v[6], w6);
+  v[7] = cmul(v[7], w7);
+  v[9] = cmul(v[9], cmul(bp[0], bp[3]));
+  v[10] = cmul(v[10], cmul(bp[1], bp[3]));
+  v[11] = cmul(v[11], cmul(w3, bp[3]));
+  v[12] = cmul(v[12], cmul(bp[2], bp[3]));
+  v[13] = cmul(v[13], cmul(w5, bp[3]));
+  v[14] = cmul(v[14], cmul(w6, bp[3]));
+  v[15] = cmul(v[15], cmul(w7, bp[3]));
+}
+
 // LDS index with one pad slot per 16 (breaks the power-of-two strides of the passes)
 __device__ __forceinline__ int lp(int i) { return i + (i >> 4); }
 
@@ -535,8 +557,13 @@ __device__ __forceinline__ void stockham_pass(v2f *v, int t, int N, int Ns,
     for (int r = 0; r < R; ++r) w[r] = v[u + B * r];
     if (Ns > 1) {
       const int ts = k * (N / (R * Ns));
+      if constexpr (R == 16) {  // W^(r ts) from the four table powers W^ts, W^2ts, W^4ts, W^8ts
+        const v2f bp[4] = {tw[ts], tw[2 * ts], tw[4 * ts], tw[8 * ts]};
+        apply_powers(w, bp);
+      } else {
 #pragma unroll
-      for (int r = 1; r < R; ++r) w[r] = cmul(w[r], tw[r * ts]);
+        for (int r = 1; r < R; ++r) w[r] = cmul(w[r], tw[r * ts]);
+      }
     }
     dft<R>(w);
 #pragma unroll
@@ -830,28 +857,6 @@ struct Dif {
   static constexpr int WAVES_PRUNE = N <= 2048 ? WELCH_DIF_WAVES_SMALL : N == 4096 ? WELCH_DIF_WAVES : 2;
   static constexpr int WAVES_FULL = N <= 2048 ? WELCH_DIF_WAVES_SMALL : 2;
 };
-
-// v[r] *= b^r, r = 1..15, from bp = {b, b^2, b^4, b^8}: each power applied as soon as it
-// is formed (at most eight of them live)
-__device__ __forceinline__ void apply_powers(v2f *v, const v2f *bp) {
-  v[1] = cmul(v[1], bp[0]);
-  v[2] = cmul(v[2], bp[1]);
-  v[4] = cmul(v[4], bp[2]);
-  v[8] = cmul(v[8], bp[3]);
-  const v2f w3 = cmul(bp[0], bp[1]), w5 = cmul(bp[0], bp[2]), w6 = cmul(bp[1], bp[2]);
-  const v2f w7 = cmul(w3, bp[2]);
-  v[3] = cmul(v[3], w3);
-  v[5] = cmul(v[5], w5);
-  v[6] = cmul(v[6], w6);
-  v[7] = cmul(v[7], w7);
-  v[9] = cmul(v[9], cmul(bp[0], bp[3]));
-  v[10] = cmul(v[10], cmul(bp[1], bp[3]));
-  v[11] = cmul(v[11], cmul(w3, bp[3]));
-  v[12] = cmul(v[12], cmul(bp[2], bp[3]));
-  v[13] = cmul(v[13], cmul(w5, bp[3]));
-  v[14] = cmul(v[14], cmul(w6, bp[3]));
-  v[15] = cmul(v[15], cmul(w7, bp[3]));
-}
 
 // bin of slot q after the last stage (digits reversed)
 template <int N>
