@@ -836,7 +836,13 @@ __global__ __launch_bounds__(MAXT) void welch_rows2_kernel(const v2f *__restrict
 #define WELCH_DIF_WAVES 3  // waves per SIMD the registers are cut for (PRUNE, N = 4096)
 #endif
 #ifndef WELCH_DIF_WAVES_SMALL
-#define WELCH_DIF_WAVES_SMALL 3  // the same for N <= 2048 (both forms)
+#define WELCH_DIF_WAVES_SMALL 3  // the same for N <= 2048 (full form)
+#endif
+#ifndef WELCH_DIF_WAVES_SMALL_PRUNE
+#define WELCH_DIF_WAVES_SMALL_PRUNE 4  // N <= 2048, PRUNE: 4 waves/SIMD (cfg1: 4096 one-wave
+#endif                                 // frames fill the GPU's 4096 slots in one round)
+#ifndef WELCH_DIF_PF_SMALL_PRUNE
+#define WELCH_DIF_PF_SMALL_PRUNE 4  // prefetch of that form (fits 128 VGPRs)
 #endif
 __host__ __device__ constexpr int dif_slot(int i) { return i + (i >> 4); }  // conflict-free strides 1, 16, 17
 
@@ -853,8 +859,9 @@ struct Dif {
   static constexpr int NW = (T + 63) / 64;           // waves per frame
   static constexpr int SLOTS = dif_slot(N - 1) + 1;  // LDS image per frame (v2f)
   static constexpr int PF = N <= 2048 ? WELCH_DIF_PF_SMALL : WELCH_DIF_PF;
+  static constexpr int PF_PRUNE = N <= 2048 ? WELCH_DIF_PF_SMALL_PRUNE : WELCH_DIF_PF;
   // waves per SIMD the registers are cut for
-  static constexpr int WAVES_PRUNE = N <= 2048 ? WELCH_DIF_WAVES_SMALL : N == 4096 ? WELCH_DIF_WAVES : 2;
+  static constexpr int WAVES_PRUNE = N <= 2048 ? WELCH_DIF_WAVES_SMALL_PRUNE : N == 4096 ? WELCH_DIF_WAVES : 2;
   static constexpr int WAVES_FULL = N <= 2048 ? WELCH_DIF_WAVES_SMALL : 2;
 };
 
@@ -874,7 +881,7 @@ __global__ __launch_bounds__(Dif<N>::NT, PRUNE ? Dif<N>::WAVES_PRUNE : Dif<N>::W
 void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__restrict__ win,
                       const v2f *__restrict__ tw, WelchGeom g, float *__restrict__ rows, int frames) {
   using D = Dif<N>;
-  constexpr int T = D::T, PF = D::PF;
+  constexpr int T = D::T, PF = PRUNE ? D::PF_PRUNE : D::PF;
   extern __shared__ v2f dyn_sh[];
   __shared__ v2f red[D::FPB][2][D::NW];  // wave partial sums of the segment mean, by parity
   const int fl = D::FPB == 1 ? 0 : (int)threadIdx.x / T;  // frame within the workgroup
