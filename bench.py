@@ -9,13 +9,20 @@ waterfall row-roll of all F lines (Waterfall.image_update, S:1638-1664).
 Workload (BASELINE.json configs[1]): 2.4 MS/s synthetic IQ, N_FFT=4096, zoom=8, fp32,
 W=512, L = fft_avg*N = 73*4096 = 299,008 samples per line (fft_avg = int(fs/N/8), S:1546).
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N`): frames are independent, so every
-rank processes its own F frames on its own GPU with no data-path collective (weak
-scaling); the barrier and the max-over-ranks time are the only collectives.
+Multi-GPU: frames are independent (S:2091-2111, T:1516-1538), so every rank processes its
+own F frames on its own GPU with no data-path collective (weak scaling).  Under
+torch.distributed.run the ranks come from the environment; `--gpus N` without it spawns N
+rank processes itself (before anything touches a GPU).  The barrier and the max-over-ranks
+time go through gloo on the host: no RCCL on this path.
+
+Outside the timed region: per-launch HIP-event times (the dominant kernel's roofline), a
+parity check of sampled frames against the float64 oracle (checker only), and the
+end-to-end host path (single-frame latency; streaming from pinned host memory with the H2D
+copy of batch k+1 overlapping the compute of batch k).
 
 CPU baseline: the reference's numpy/scipy library path (oracle/scipy_path.py, the same
-decimate/welch calls) on a bounded sample of frames, rank 0 at N=1 only, run in a
-spawn-context process pool BEFORE the GPU is touched.
+decimate/welch calls) on a bounded sample of frames, rank 0 at N=1 only, in a spawn-context
+process pool of the job's CPU share, run BEFORE the GPU is touched.
 """
 from __future__ import annotations
 
@@ -23,6 +30,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,13 +57,35 @@ CONFIGS = {
 }
 IN_BYTES = {"complex64": 8, "complex32": 4, "cu8": 2}
 TONES = ((0.31, 1.0), (-0.57, 0.1))
+# plan launch name -> kernel-name prefix in the rocprofv3 / PMC summaries
+KERNEL_OF = {"xa_stage_mix": "xa_stage_kernel<true", "xa_stage": "xa_stage_kernel<false",
+             "welch_rows": "welch_", "welch4": "welch4_"}
+
+
+def alg_bytes_per_line(bps: int, L: int, W: int) -> int:
+    """bps*L of IQ in + 4*W row out + 4*W waterfall ring row."""
+    return bps * L + 8 * W
 
 
 # ----------------------------------------------------------------------------- CPU leg
+def cpu_share() -> tuple:
+    """(cores, how): the CPUs this job may use -- the cgroup quota, else OMP_NUM_THREADS
+    (the GPU box sets it to the job's share), else the affinity mask."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(p))), "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        return int(os.environ["OMP_NUM_THREADS"]), "OMP_NUM_THREADS (the job's CPU share)"
+    return len(os.sched_getaffinity(0)), "sched_getaffinity"
+
+
 def _cpu_worker(args):
     """Runs in a spawned process: time the reference's library path on fresh frames."""
     cfg, seconds, seed = args
-    import numpy as np  # noqa: F401
+    os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import scipy_path
     from pypanadapter_amd import synth
     L = cfg["n_fft"] * cfg["n_avg"]
@@ -70,34 +101,69 @@ def _cpu_worker(args):
             return n, el
 
 
-def cpu_baseline(cfg, seconds: float, workers: int):
+def cpu_baseline(cfg, seconds: float, workers: int, how: str):
     import multiprocessing as mp
     L = cfg["n_fft"] * cfg["n_avg"]
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
     ctx = mp.get_context("spawn")
-    # single core
-    n1, t1 = _cpu_worker((cfg, max(2.0, seconds / 3), 11))
+    n1, t1 = _cpu_worker((cfg, max(2.0, seconds / 3), 11))  # one core
     single = n1 * L / t1 / 1e6
-    # all worker processes, one frame stream each
     t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
+    with ctx.Pool(workers) as pool:  # one frame stream per worker process
         res = pool.map(_cpu_worker, [(cfg, seconds, 100 + i) for i in range(workers)])
     wall = time.perf_counter() - t0
     frames = sum(r[0] for r in res)
     span = max(r[1] for r in res)
-    value = frames * L / span / 1e6
     try:
         model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo")
                  if ln.startswith("model name")][0]
-    except Exception:
+    except (OSError, IndexError):
         model = "unknown"
-    return {"value": round(value, 3), "unit": "MS/s", "cores": workers, "kind": "port",
-            "lines_per_s": round(frames / span, 2),
+    return {"value": round(frames * L / span / 1e6, 3), "unit": "MS/s", "cores": workers,
+            "kind": "port", "lines_per_s": round(frames / span, 2),
             "single_core_MS_per_s": round(single, 3),
+            "single_core_ms_per_frame": round(t1 / n1 * 1e3, 2),
             "sample": (f"oracle/scipy_path.psd_row (the reference's decimate/welch/fftshift/log10 "
                        f"library calls) on {frames} frames of L={L} complex64 in {workers} spawned "
-                       f"processes for ~{seconds:.0f}s each (+1 core for {t1:.1f}s); "
-                       f"wall {wall:.1f}s; host {model}, os.cpu_count()={os.cpu_count()}")}
+                       f"processes for ~{seconds:.0f}s each (+1 core for {t1:.1f}s); wall {wall:.1f}s; "
+                       f"cores = {how}; host {model}, os.cpu_count()={os.cpu_count()}")}
+
+
+def parity_check(frames: dict, rows: dict, cfg, f_lo: float) -> dict:
+    """Checker only: sampled frames of the timed batch against the float64 oracle under the
+    fp32 gate (|ddB| <= 1e-3 within 100 dB of the peak, |d amp| <= 1e-5 peak)."""
+    import numpy as np
+    from oracle import coracle
+    coracle.build()
+    N, z = cfg["n_fft"], cfg["zoom"]
+    W = N // z
+    worst_db = worst_amp = 0.0
+    for f, x in frames.items():
+        ref = coracle.psd_row(x, cfg["fs"], N, z, W, f_lo=f_lo)
+        row = rows[f].astype(np.float64)
+        pk = ref.max()
+        m = ref > pk - 100.0
+        worst_db = max(worst_db, float(np.abs(row - ref)[m].max()))
+        worst_amp = max(worst_amp, float(np.abs(10 ** (row / 20) - 10 ** (ref / 20)).max() / 10 ** (pk / 20)))
+    return {"frames": sorted(frames), "max_abs_ddb_within_100dB": worst_db, "max_amp_err_rel_peak": worst_amp,
+            "gate": "|ddB| <= 1e-3 within 100 dB of peak and |d amp| <= 1e-5 x peak",
+            "pass": bool(worst_db <= 1e-3 and worst_amp <= 1e-5)}
+
+
+# ----------------------------------------------------------------------------- launcher
+def spawn_ranks(argv) -> int:
+    """`--gpus N` outside torch.distributed.run: N rank processes, one per GPU, started
+    before this process touches any GPU; returns the worst exit code."""
+    n = int(argv.gpus)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    return max(abs(p.wait()) for p in procs)
 
 
 # ----------------------------------------------------------------------------- GPU leg
@@ -118,25 +184,123 @@ def make_frames(torch, F, L, cfg, device, seed):
     return x
 
 
+def encode(torch, x, in_dtype):
+    """Device frames in the plan's input format (complex32 = fp16 I,Q; cu8 = RTL-SDR bytes)."""
+    if in_dtype == "complex32":
+        return x.to(torch.float16).contiguous()
+    if in_dtype == "cu8":
+        return torch.clamp(torch.round(127.5 + 127.5 * 0.25 * x), 0, 255).to(torch.uint8).contiguous()
+    return x
+
+
+def decoded_host(torch, xe, f, in_dtype):
+    """Frame f exactly as the kernels read it, complex128 on the host (for the checker)."""
+    import numpy as np
+    a = xe[f].cpu().numpy()
+    if in_dtype == "cu8":
+        a = (a.astype(np.float64) - 127.5) / 127.5
+    a = a.astype(np.float64)
+    return a[:, 0] + 1j * a[:, 1]
+
+
+def stamped_profile(path, F, in_dtype):
+    """A committed profile summary, if it was measured on these kernel sources."""
+    from pypanadapter_amd import build
+    try:
+        tj = json.load(open(path))
+    except (OSError, ValueError):
+        return None, "absent"
+    if tj.get("source_hash") != build.source_hash():
+        return None, f"stale (measured on sources {tj.get('source_hash')}, now {build.source_hash()})"
+    if tj.get("frames") != F or tj.get("in_dtype", "complex64") != in_dtype:
+        return None, "other workload"
+    return tj, "ok"
+
+
+def end_to_end(torch, args, cfg, x_dev, dev):
+    """Host-path numbers (PCIe-inclusive; never `value`): single-frame psd latency as the
+    reference calls it (one chunk per update(), S:2102), and streaming throughput from pinned
+    host memory through zfft_process (batched, H2D of batch k+1 under compute of batch k)."""
+    import numpy as np
+    from pypanadapter_amd import ZoomFFT, synth
+    N, z, fs = cfg["n_fft"], cfg["zoom"], cfg["fs"]
+    L, W = N * cfg["n_avg"], N // z
+    out = {}
+    x1 = synth.make_iq(L, fs, 4242, n_fft=N, zoom=z, n_win=W)
+    with ZoomFFT(N, z, fs, n_win=W, device=dev.index) as plan:
+        for _ in range(3):
+            plan.rows(x1)
+        lat = []
+        for _ in range(40):
+            t0 = time.perf_counter()
+            plan.rows(x1)
+            lat.append((time.perf_counter() - t0) * 1e3)
+    lat = np.sort(lat)
+    out["single_frame_latency_ms"] = {"p50": round(float(np.percentile(lat, 50)), 3),
+                                      "p99": round(float(np.percentile(lat, 99)), 3),
+                                      "what": "psd_row of one host complex64 frame (H2D, decimate, "
+                                              "Welch, D2H) through zfft_process"}
+    Fs = min(args.e2e_frames, x_dev.shape[0])
+    stream = {}
+    for fmt in ("complex64", "cu8"):
+        xe = encode(torch, x_dev[:Fs], fmt)
+        host = torch.empty(xe.shape, dtype=xe.dtype, pin_memory=True)
+        host.copy_(xe)
+        nbytes = host.numel() * host.element_size()
+        tmp = torch.empty_like(xe)  # the PCIe H2D ceiling: a plain pinned -> device copy
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            tmp.copy_(host, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        h2d = 3 * nbytes / (time.perf_counter() - t0) / 1e9
+        del tmp
+        rows = np.empty((Fs, W), np.float32)
+        with ZoomFFT(N, z, fs, n_win=W, device=dev.index, in_dtype=fmt) as plan:
+            plan.process_host(host.data_ptr(), L, Fs, rows.ctypes.data)
+            reps = 3
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                plan.process_host(host.data_ptr(), L, Fs, rows.ctypes.data)
+            el = (time.perf_counter() - t0) / reps
+        rate = Fs * L / el / 1e6
+        bound = h2d * 1e3 / IN_BYTES[fmt]
+        stream[fmt] = {"MS_per_s": round(rate, 1), "lines_per_s": round(Fs / el, 1),
+                       "frames": Fs, "bytes_per_sample": IN_BYTES[fmt],
+                       "pcie_h2d_GBps": round(h2d, 1), "pcie_bound_MS_per_s": round(bound, 1),
+                       "frac_of_pcie_bound": round(rate / bound, 3)}
+        del host, xe
+    out["streaming_pinned"] = stream
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=200, help="timed steps (default: >= 1 s at cfg2)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per rank (default: config)")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--warm", type=int, default=0)
     ap.add_argument("--path", type=int, default=0,
-                    help="0 auto, 1 exact order, 2 fused interior, 3 DF2T exact tiles, 4 XA tiles")
+                    help="0 auto, 1 exact order, 2 fused interior, 3 XA tiles")
     ap.add_argument("--welch", type=int, default=0,
                     help="Welch kernel: 0 auto, 1 one workgroup per frame, 2 four-step (A/B runs)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0: the job's CPU share")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--e2e-frames", type=int, default=1024)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank/launcher check only: no GPU call (CPU tests of --gpus N)")
     ap.add_argument("--in-dtype", default="complex64", choices=sorted(IN_BYTES),
                     help="IQ storage format in HBM (cfg5: complex32 = fp16)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
 
     cfg = dict(CONFIGS[args.config])
     F = args.frames or cfg["frames"]
@@ -149,16 +313,29 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-        cpu = cpu_baseline(cfg, args.cpu_seconds, workers)
+        share, how = cpu_share()
+        workers = args.cpu_workers or share
+        cpu = cpu_baseline(cfg, args.cpu_seconds, workers, how if not args.cpu_workers else "--cpu-workers")
 
     import torch
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     dist = None
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        import torch.distributed as dist  # gloo on the host: barrier + max-reduce only
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.dry_run:  # the launcher's contract without touching a GPU
+        me = torch.tensor([rank, local, world, os.getpid()], dtype=torch.int64)
+        allr = [torch.zeros(4, dtype=torch.int64) for _ in range(world)] if dist else [me]
+        if dist:
+            dist.all_gather(allr, me)
+            dist.barrier()
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "world": world,
+                              "ranks": [dict(zip(("rank", "local_rank", "world", "pid"), map(int, r)))
+                                        for r in allr]}))
+        return
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
 
     from pypanadapter_amd import ZoomFFT
     f_lo = 1.0 + cfg.get("lo_step", 0.0) * rank
@@ -170,18 +347,17 @@ def main():
     if args.welch:
         plan.set_welch(args.welch)
     stream = torch.cuda.Stream(dev)  # a real stream: the null stream's handle (0) would be
-    torch.cuda.set_stream(stream)    # read by the C-ABI as "the plan's own stream"
+    torch.cuda.set_stream(stream)    # read by the C-ABI as HIP's default stream
     sp = stream.cuda_stream
     x = make_frames(torch, F, L, cfg, dev, 1234 + rank)
-    if args.in_dtype == "complex32":
-        x = x.to(torch.float16).contiguous()
-    elif args.in_dtype == "cu8":
-        x = torch.clamp(torch.round(127.5 + 127.5 * 0.25 * x), 0, 255).to(torch.uint8).contiguous()
+    xe = encode(torch, x, args.in_dtype)
+    if xe is not x and (args.no_e2e or rank != 0):
+        x = None  # only the e2e leg re-encodes from the float frames
     rows = torch.empty((F, W), dtype=torch.float32, device=dev)
     torch.cuda.synchronize(dev)
 
     def step():
-        plan.process_device(x.data_ptr(), L, F, rows.data_ptr(), sp)
+        plan.process_device(xe.data_ptr(), L, F, rows.data_ptr(), sp)
         plan.waterfall_push_device(rows.data_ptr(), F, sp)
 
     for _ in range(args.warmup):
@@ -202,56 +378,65 @@ def main():
     if dist:
         dist.barrier()
     gpu_ms = ev0.elapsed_time(ev1)
-    t = torch.tensor([wall, gpu_ms / 1e3], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, gpu_ms / 1e3], dtype=torch.float64)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, ev_max = float(t[0]), float(t[1])
 
-    # per-launch breakdown from one instrumented step (events on the launch stream)
+    # per-launch HIP-event times (events on the launch stream) over a few instrumented steps
     plan.set_timing(True)
-    plan.process_device(x.data_ptr(), L, F, rows.data_ptr(), sp)
-    launch_ms = plan.timings()
+    acc, n_inst = {}, max(1, min(args.steps, 10))
+    for _ in range(n_inst):
+        plan.process_device(xe.data_ptr(), L, F, rows.data_ptr(), sp)
+        for i, (nm, ms) in enumerate(zip(plan.launch_names(), plan.timings())):
+            acc[f"{i}:{nm}"] = acc.get(f"{i}:{nm}", 0.0) + ms
     plan.set_timing(False)
     torch.cuda.synchronize(dev)
+    kernels = {k: round(v / n_inst, 4) for k, v in acc.items()}
     finite = bool(torch.isfinite(rows).all().item())
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
+    check = None
+    if not args.no_check:
+        pick = sorted({0, F // 2, F - 1})
+        host_rows = rows.cpu().numpy()
+        frames = {f: decoded_host(torch, xe, f, args.in_dtype) for f in pick}
+        check = parity_check(frames, {f: host_rows[f] for f in pick}, cfg, f_lo)
+    e2e = None
+    if not args.no_e2e:
+        plan.close()
+        del rows
+        e2e = end_to_end(torch, args, cfg, x if x is not None else xe, dev)
+
     ms_per_step = wall_max / args.steps * 1e3
     total_samples = F * L * args.steps * world
     value = total_samples / wall_max / 1e6
     lines = F * args.steps * world / wall_max
     bps = IN_BYTES[args.in_dtype]
-    alg_bytes_step = F * (bps * L + 8 * W)  # bps*L in + 4*W row + 4*W ring row
+    alg_step = F * alg_bytes_per_line(bps, L, W)
     ev_ms_step = ev_max / args.steps * 1e3
-    achieved = alg_bytes_step / (ev_ms_step / 1e3) / 1e9
-    names = plan.launch_names()
-    kernels = {}
-    for i, (nm, ms) in enumerate(zip(names, launch_ms)):
-        kernels[f"{i}:{nm}"] = round(ms, 4)
+    path_gbs = alg_step / (ev_ms_step / 1e3) / 1e9
     dominant = max(kernels, key=lambda k: kernels[k]) if kernels else None
-    dom_roof = None
-    if dominant is not None and "stage_mix" in dominant:
-        # the stage-0 decimator: reads the caller's IQ (bps*L per frame), writes the first
-        # decimated stage (complex64, ceil(L/2) per frame)
-        dom_bytes = F * (bps * L + 8 * ((L + 1) // 2))
-        dom_gbs = dom_bytes / (kernels[dominant] / 1e3) / 1e9
-        dom_roof = {"kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes,
-                    "achieved": round(dom_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(dom_gbs / HBM_PEAK_GBS, 4), "launch_ms": kernels[dominant]}
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            if (tj.get("frames") == F and tj.get("in_dtype", "complex64") == args.in_dtype
-                    and tj.get("schedule") == "xa"  # measured on the current auto schedule
-                    and not args.path and not args.welch and not args.block and not args.warm):
-                traffic = tj.get("hbm_bytes_per_step")
-        except Exception:
-            traffic = None
+    traffic_j, traffic_status = stamped_profile(
+        os.path.join(ROOT, "profiles", f"traffic_{args.config}.json"), F, args.in_dtype)
+    sq_j, sq_status = stamped_profile(os.path.join(ROOT, "profiles", f"sq_{args.config}.json"), F,
+                                      args.in_dtype)
+    default_sched = not (args.path or args.welch or args.block or args.warm)
+    dom_traffic = step_traffic = valu = None
+    if dominant is not None and default_sched:
+        pref = KERNEL_OF.get(dominant.split(":", 1)[1], "?")
+        if traffic_j:
+            step_traffic = traffic_j.get("hbm_bytes_per_step")
+            dom_traffic = sum(v["hbm_bytes_per_step_fetch_x2"] for k, v in traffic_j["per_kernel"].items()
+                              if k.startswith(pref)) or None
+        if sq_j:
+            vk = [v for k, v in sq_j["per_kernel"].items() if k.startswith(pref)]
+            valu = vk[0].get("valu_busy") if vk else None
+    dom_ms = kernels.get(dominant) if dominant else None
+    dom_gbs = alg_step / (dom_ms / 1e3) / 1e9 if dom_ms else None
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -268,17 +453,25 @@ def main():
         "config": {"workload": f"{args.config}: {cfg['desc']}", "n_fft": N, "zoom": zoom,
                    "n_win": W, "samples_per_line": L, "frames_per_rank": F, "fs": fs,
                    "window": "hamming", "in_dtype": args.in_dtype, "f_lo_rank0": 1.0,
-                   "parallelism": f"frame-sharded x{world}, no collective"},
+                   "parallelism": f"frame-sharded x{world}, no collective (gloo barrier only)"},
         "lines_per_s": round(lines, 1),
-        "roofline": {"bound": "hbm", "kernel": "IQ->log-PSD path (all launches of one step)",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_step": alg_bytes_step,
-                     "event_ms_per_step": round(ev_ms_step, 4)},
+        "roofline": {"bound": "hbm", "kernel": dominant,
+                     "achieved": round(dom_gbs, 1) if dom_gbs else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(dom_gbs / HBM_PEAK_GBS, 4) if dom_gbs else None,
+                     "traffic": dom_traffic,
+                     "algorithmic_bytes_per_launch": alg_step,
+                     "bytes_basis": "SURVEY §8(d) per line (bps*L IQ in + 4W row + 4W ring row) x F lines "
+                                    "per launch; intermediates excluded",
+                     "avg_launch_ms": dom_ms, "valu_util": valu,
+                     "profiles": {"traffic": traffic_status, "sq": sq_status}},
+        "path_roofline": {"what": "whole IQ->log-PSD->waterfall step (all launches)",
+                          "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(path_gbs / HBM_PEAK_GBS, 4), "traffic": step_traffic,
+                          "event_ms_per_step": round(ev_ms_step, 4)},
         "kernels": kernels,
-        "dominant_kernel": dominant,
-        "dominant_roofline": dom_roof,
         "rows_finite": finite,
+        "parity_checked_frames": check,
+        "end_to_end": e2e,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out))

@@ -69,7 +69,8 @@ enum zfft_window_kind {
 typedef struct zfft_config {
   int32_t n_fft;           /* N: power of two, 32..65536 (AppState.fft_size, S:1397; cfg5)  */
   int32_t zoom;            /* power of two, 1..512 (AppState.fft_ratio, S:2079-2086)        */
-  int32_t n_win;           /* W: row length, even, 2..N (N_WIN S:1757; T:1542)              */
+  int32_t n_win;           /* W: row stride, 2..N (N_WIN S:1757; T:1542); odd W gives the
+                              reference's W - 1 entries (zfft_plan_row_length)            */
   int32_t window_kind;     /* enum zfft_window_kind                                         */
   double fs;               /* sample rate, Hz (panadapter.SampleRate)                       */
   double f_lo;             /* LO frequency, Hz; the reference hard-codes 1.0 (S:2090)       */
@@ -93,9 +94,11 @@ typedef struct zfft_plan zfft_plan;
 int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_plan **out);
 int zfft_plan_destroy(zfft_plan *plan);
 int zfft_plan_config(const zfft_plan *plan, zfft_config *out);  /* the configuration in use */
-/* Valid floats per row (rows keep the stride n_win): n_win, except for real input
- * (in_dtype 3) at zoom 1, where the reference's welch is one-sided and its
- * fftshift(P)[N/2 - W/2 : N/2 + W/2] slice of the N/2+1 bins is shorter. */
+/* Valid floats per row (rows keep the stride n_win): the length of the reference's slice
+ * fftshift(P)[N//2 - W//2 : N//2 + W//2] (S:2114), i.e. n_win rounded down to even, except
+ * for real input (in_dtype 3) at zoom 1, where the reference's welch is one-sided and that
+ * slice of the N/2+1 bins is shorter.  A waterfall of any width >= 40/60
+ * (the one-sided rows are odd) is a plan with n_win = that width. */
 int zfft_plan_row_length(const zfft_plan *plan);
 
 /* Host-buffer path: n_frames frames of n_samples IQ each (frame-major), rows_out holds
@@ -182,11 +185,13 @@ int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *coun
 /* Comma-separated names of the intervals zfft_plan_timings returns (owned by the plan). */
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
-/* Decimator schedule: 0 = automatic (3 for batches of >= 256 frames, else 2 where the frame
- * is long enough for its edge windows, else 1), 1 = blocked warm-up passes in the reference order,
- * 2 = fused commuted-order interior + exact edge windows, 3 = exact tiles (one wave per
- * frame, state scans, no intermediate in memory).  All produce the reference's rows within
- * the fp32 parity gate; diagnostics / A-B only. */
+/* Decimator schedule: 0 = automatic (3 for batches of >= 1024 frames, or >= 512 frames of
+ * <= 2^19 samples; otherwise 2 where the frame is long enough for its edge windows, else 1),
+ * 1 = blocked warm-up passes in the reference order (frames split over many waves),
+ * 2 = blocked, fused commuted-order interior + exact edge windows, 3 = XA tiles (one wave per
+ * frame: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned, no
+ * intermediate in memory).  All produce the reference's rows within the fp32 parity gate;
+ * diagnostics / A-B only (zfft_plan.cpp auto_xa, use_fused). */
 int zfft_plan_path(zfft_plan *plan, int32_t path);
 
 /* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 16384, four-step

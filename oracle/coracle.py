@@ -89,14 +89,14 @@ def window(window, nperseg: int) -> np.ndarray:
 
 
 def welch_row(x: np.ndarray, fs: float, n_fft: int, n_win: int, win="hamming") -> np.ndarray:
-    """S:2111-2119 -> float64 dB row of length n_win."""
+    """S:2111-2119 -> float64 dB row: the slice [N//2 - W//2, N//2 + W//2), 2 (W//2) long."""
     lib = _load()
     x = np.ascontiguousarray(x, dtype=np.complex128)
     nperseg = min(n_fft, len(x))
     w = win if isinstance(win, np.ndarray) else window(win, nperseg)
     w = np.ascontiguousarray(w, dtype=np.float64)
     assert len(w) == nperseg
-    row = np.empty(n_win, dtype=np.float64)
+    row = np.empty(n_win & ~1, dtype=np.float64)
     rc = lib.oracle_welch_row(_ptr(x), len(x), fs, n_fft, n_win, _ptr(w), nperseg, _ptr(row))
     if rc:
         raise ValueError(f"oracle_welch_row failed ({rc})")

@@ -157,7 +157,8 @@ static void fft_c(cplx *v, int N) {
 /*
  * Welch + fftshift/crop + 20*log10: S:2111-2119.  x complex128 interleaved, length Ld.
  * win has length nperseg = min(n_fft, Ld) (_triage_segments: short input -> nperseg = Ld).
- * row[j] = 20*log10(P[(j - W/2) mod N]), j in [0, W).
+ * row[j] = 20*log10(P[(j - W//2) mod N]), j in [0, 2 (W//2)): the slice
+ * fftshift(P)[N//2 - W//2 : N//2 + W//2] (W - 1 entries for odd W).
  */
 int oracle_welch_row(const double *x, int64_t Ld, double fs, int n_fft, int n_win,
                      const double *win, int nperseg, double *row) {
@@ -189,7 +190,7 @@ int oracle_welch_row(const double *x, int64_t Ld, double fs, int n_fft, int n_wi
     for (int k = 0; k < n_fft; ++k) acc[k] += buf[k].re * buf[k].re + buf[k].im * buf[k].im;
   }
   double scale = 1.0 / (fs * wss);
-  for (int j = 0; j < n_win; ++j) {
+  for (int j = 0; j < (n_win & ~1); ++j) {
     int k = ((j - n_win / 2) % n_fft + n_fft) % n_fft;
     double p = acc[k] * scale / (double)nseg;
     row[j] = 20.0 * log10(fabs(p));

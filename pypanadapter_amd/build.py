@@ -9,7 +9,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libzfft.so")
-SOURCES = ["zfft_kernels.hip", "xt_kernels.hip", "xa_kernels.hip", "zfft_plan.cpp", "zfft_ring.cpp",
+SOURCES = ["zfft_kernels.hip", "xa_kernels.hip", "zfft_plan.cpp", "zfft_ring.cpp",
            "windows.cpp"]
 HEADERS = ["zfft_internal.h", "zfft_device.h", "cheby1_q2.h", os.path.join("..", "..", "include", "zfft.h")]
 ARCH = os.environ.get("ZFFT_OFFLOAD_ARCH", "gfx950")
@@ -43,6 +43,17 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH,
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
     return out
+
+
+def source_hash() -> str:
+    """Digest of the kernel/library sources: profiles measured on other sources (PMC traffic,
+    SQ counters) are stamped with it, and bench.py uses them only while it still matches."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in sorted(SOURCES + HEADERS):
+        with open(os.path.join(CSRC, name), "rb") as fh:
+            h.update(name.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
 
 
 if __name__ == "__main__":

@@ -72,27 +72,6 @@ struct FusedGeom {
 hipError_t launch_fused_pass(const float2 *in, float2 *out, bool desc, bool two, bool nat,
                              const FusedGeom &g, int frames, hipStream_t st);
 
-// Exact-tile decimation stage (xt_kernels.hip): one wave per frame, tiles of 64 lanes x
-// kXtB samples, lane states scanned in the real modal basis of the cascade's state matrix
-// A (4 rotation-scaling modes, one per section pole pair).  fp64 on the host -> fp32.
-constexpr int kXtB = 16;
-constexpr int kXtT = 64 * kXtB;
-constexpr int kXtScan = 5;          // scan levels of the slowest mode (radius 0.9351)
-constexpr int kXtHeld = kXtB / 2;   // kept (decimated) outputs per lane and tile
-struct XtModal {
-  float ti[8][8];          // T^-1: DF2T state (z0_0 z1_0 z0_1 ...) -> modal (a0 b0 a1 b1 ...)
-  float zim[8];            // T^-1 zi: steady state per unit input (sosfilt_zi)
-  float cm[kXtB][8];       // C A^t T: output t samples after a modal state
-  float p16[4][2];         // lambda_j^16 (re, im): one lane sub-block
-  float scan[kXtScan][4][2];  // lambda_j^(16 * 2^d): scan level d
-  float lag[64][4][2];     // lambda_j^(16 i): i sub-blocks down from the tile top
-  float wt[kXtB][2];       // exp(-2 pi i f_lo t / fs), t < 16: the LO across one sub-block
-  Sos32 sos;               // the cascade, read per pass (not pinned in SGPRs for the kernel)
-};
-
-hipError_t launch_xt_stage(const InDesc &in, int n, const float2 *lo, bool mix,
-                           float2 *out, int frames, const XtModal *tab, hipStream_t st);
-
 // "XA" decimation stage (xa_kernels.hip; design model tools/xa_proto.py).  The cascade
 // H = N(z)/D(z), N = b0 (1+z^-1)^8, is run as a forward all-pole cascade 1/D(z) at the
 // input rate, a 25-tap FIR M = N(z) N(1/z) D(-1/z) evaluated only at the kept (odd)

@@ -434,7 +434,7 @@ __device__ __forceinline__ int welch_slot(const WelchGeom &g, int k, float &mult
   mult = 1.f;
   if (!g.onesided) {
     const int j = (k + (g.n_win >> 1)) & (g.n_fft - 1);
-    return j < g.n_win ? j : -1;
+    return j < (g.n_win & ~1) ? j : -1;  // odd W: the reference's slice has W - 1 entries
   }
   const int h = g.n_fft >> 1, M = h + 1;
   if (k > h) return -1;
@@ -687,114 +687,6 @@ __global__ __launch_bounds__(MAXT, (MAXT == 256 ? WELCH_MINB : 1)) void welch_ro
     __syncthreads();  // LDS reads of this segment done before the next one writes
   }
   // bins owned by this thread: output positions of the last pass
-  if (!act) return;
-  float *__restrict__ row = rows + (int64_t)f * g.n_win;
-  const int lastNs = N == R0 ? 1 : N / 16;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k = N == R0 ? stockham_out_index<R0>(t, N, 1, i) : stockham_out_index<16>(t, N, lastNs, i);
-    float mult;
-    const int j = welch_slot(g, k, mult);
-    if (j >= 0) row[j] = 20.f * log10f(acc[i] * g.scale * mult);
-  }
-}
-
-// Welch row, v2 (N <= 8192): the same FFT, with the barriers per segment cut from five to
-// two.  The constant-detrend mean of segment s+1 is reduced while segment s is transformed
-// (its samples are the prefetched registers; the partial sums ride on segment s's LDS
-// barriers), and the Stockham passes ping-pong between two LDS images, so the next
-// segment's first store needs no barrier of its own.  Detrending stays in the time domain
-// before the window, as scipy's detrend='constant' (_spectral_py.py _spectral_helper).
-template <int R0, int MAXT>
-__global__ __launch_bounds__(MAXT) void welch_rows2_kernel(const v2f *__restrict__ x, int64_t len,
-                                                           const float *__restrict__ win,
-                                                           const v2f *__restrict__ tw, WelchGeom g,
-                                                           float *__restrict__ rows, int frames) {
-  extern __shared__ v2f sh[];
-  const int N = g.n_fft, T = blockDim.x, t = threadIdx.x;
-  const int T16 = N >> 4;
-  const bool act = t < T16;
-  const int img = lp(N) + 16;
-  v2f *red = sh + 2 * img;  // [2][16] partial sums, by segment parity
-  int f = blockIdx.x;
-  if ((frames & 7) == 0 && frames >= 64)  // spread consecutive frames over the 8 XCDs evenly
-    f = (blockIdx.x & 7) * (frames >> 3) + (blockIdx.x >> 3);
-  const v2f *__restrict__ xf = x + (int64_t)f * len;
-  const int nw = (T + 63) >> 6;
-
-  auto load_seg = [&](v2f *dst, int s) {
-    const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int n = t + i * T16;
-      dst[i] = (act && n < g.nperseg) ? seg[n] : splat(0.f);
-    }
-  };
-  auto post_sum = [&](const v2f *v, int slot) {  // wave partial sums -> red[slot][wave]
-    v2f sum = splat(0.f);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sum += v[i];
-    sum = wave_sum(sum);
-    if ((t & 63) == 0) red[slot * 16 + (t >> 6)] = sum;
-  };
-  auto mean_of = [&](int slot) {  // after a barrier that follows post_sum(slot)
-    v2f q = splat(0.f);
-    for (int w = 0; w < nw; ++w) q += red[slot * 16 + w];
-    return q * (1.f / (float)g.nperseg);
-  };
-
-  v2f pf[16];
-  load_seg(pf, 0);
-  post_sum(pf, 0);
-  __syncthreads();
-  float acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  // image written next; it flips after every read, so a segment's first store never lands
-  // in the image the previous segment read last (whose readers may still be running)
-  int buf = 0;
-
-  for (int s = 0; s < g.nseg; ++s) {
-    v2f v[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = pf[i];
-    const bool more = s + 1 < g.nseg;
-    if (more) load_seg(pf, s + 1);  // in flight during this segment's FFT
-    const v2f mean = mean_of(s & 1);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {  // zero-pad slots (n >= nperseg) get window 0
-      const int n = t + i * T16;
-      v[i] = (v[i] - mean) * ((act && n < g.nperseg) ? win[n] : 0.f);
-    }
-    if (act) {
-      stockham_pass<R0>(v, t, N, 1, tw);
-      if (N > R0) stockham_store<R0>(v, sh + buf * img, t, N, 1);
-    }
-    bool posted = false;
-    for (int Ns = R0; Ns < N; Ns *= 16) {
-      if (!posted && more && Ns * 16 >= N) {  // before the last barrier: the next segment's
-        post_sum(pf, (s + 1) & 1);           // loads have had every earlier pass to land
-        posted = true;
-      }
-      __syncthreads();
-      if (act) {
-        const v2f *src = sh + buf * img;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = src[lp(t + r * T16)];
-        stockham_pass<16>(v, t, N, Ns, tw);
-        if (Ns * 16 < N) stockham_store<16>(v, sh + (buf ^ 1) * img, t, N, Ns);
-      }
-      buf ^= 1;  // read image done (after the next barrier it may be rewritten)
-    }
-    if (!posted && more) {  // N == R0: no LDS pass
-      post_sum(pf, (s + 1) & 1);
-      __syncthreads();
-    }
-    if (act) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = fmaf(v[i].x, v[i].x, fmaf(v[i].y, v[i].y, acc[i]));
-    }
-  }
   if (!act) return;
   float *__restrict__ row = rows + (int64_t)f * g.n_win;
   const int lastNs = N == R0 ? 1 : N / 16;
@@ -1391,28 +1283,6 @@ static hipError_t welch_launch_t(const float2 *x, int64_t len, const float *win,
   return hipGetLastError();
 }
 
-template <int R0, int MAXT>
-static hipError_t welch2_launch_t(const float2 *x, int64_t len, const float *win,
-                                  const float2 *tw, const WelchGeom &g, float *rows, int frames,
-                                  hipStream_t st) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)welch_rows2_kernel<R0, MAXT>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (2 * (8192 + 8192 / 16 + 16) + 32) * (int)sizeof(v2f));
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int T = g.n_fft / 16 > 64 ? g.n_fft / 16 : 64;
-  const size_t lds = (size_t)(2 * (g.n_fft + g.n_fft / 16 + 16) + 32) * sizeof(v2f);
-  hipLaunchKernelGGL((welch_rows2_kernel<R0, MAXT>), dim3(frames), dim3(T), lds, st, (const v2f *)x,
-                     len, win, (const v2f *)tw, g, rows, frames);
-  return hipGetLastError();
-}
-
-#ifndef WELCH_V2
-#define WELCH_V2 0  // v2 (mean one segment ahead, 2 barriers) measured slower on MI355X: 1.36 vs 1.19 ms at cfg2
-#endif
 #ifndef WELCH_DIF
 #define WELCH_DIF 1
 #endif
@@ -1434,8 +1304,6 @@ static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, c
       default: break;
     }
   }
-  if (WELCH_V2 && g.n_fft <= 4096) return welch2_launch_t<R0, 256>(x, len, win, tw, g, rows, frames, st);
-  if (WELCH_V2 && g.n_fft <= 8192) return welch2_launch_t<R0, 512>(x, len, win, tw, g, rows, frames, st);
   // threads = N/16 (>= 64): N <= 4096 -> <= 256 threads, room for the prefetch registers
 #ifndef WELCH_PF
 #define WELCH_PF 1

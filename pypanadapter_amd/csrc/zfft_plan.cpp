@@ -41,22 +41,8 @@ Sos32 sos32() {
 
 namespace {
 
-// ---- exact-tile tables (fp64 -> fp32), state order z0_0 z1_0 z0_1 z1_1 ... ----
+// ---- 8x8 helpers (fp64) for the modal bases of the XA cascades ----
 using Mat8 = std::vector<double>;  // 8x8 row-major
-void cascade_d(const double in[8], double u, double out[8], double *y) {
-  double s[8];
-  for (int i = 0; i < 8; ++i) s[i] = in[i];
-  double x = u;
-  for (int k = 0; k < 4; ++k) {
-    const double *c = kDecimSos[k];
-    const double yy = c[0] * x + s[2 * k];
-    s[2 * k] = c[1] * x - c[4] * yy + s[2 * k + 1];
-    s[2 * k + 1] = c[2] * x - c[5] * yy;
-    x = yy;
-  }
-  for (int i = 0; i < 8; ++i) out[i] = s[i];
-  *y = x;
-}
 Mat8 matmul8(const Mat8 &a, const Mat8 &b) {
   Mat8 c(64, 0.0);
   for (int i = 0; i < 8; ++i)
@@ -64,12 +50,6 @@ Mat8 matmul8(const Mat8 &a, const Mat8 &b) {
       for (int j = 0; j < 8; ++j) c[i * 8 + j] += a[i * 8 + k] * b[k * 8 + j];
   return c;
 }
-// Real modal basis of the cascade's state matrix A (block lower triangular: section k's
-// state is driven by the outputs of sections < k).  Mode j = the pole pair of section j,
-// lambda_j = sigma + i omega = (-a1 + i sqrt(4 a2 - a1^2)) / 2; its eigenvector v is zero on
-// sections < j, the null vector of (A_jj - lambda) on section j and found by forward
-// substitution below.  Columns (Re v, Im v) of T give T^-1 A T = diag([[sigma, omega],
-// [-omega, sigma]]), so a power of A is a per-mode complex power (tools/xt_modal_proto.py).
 using cd = std::complex<double>;
 
 void mat_inverse8(const Mat8 &a, Mat8 &inv) {
@@ -100,85 +80,6 @@ void mat_inverse8(const Mat8 &a, Mat8 &inv) {
   }
 }
 
-void xt_build_tables(XtModal &X) {
-  Mat8 A(64);
-  double C[8];
-  for (int q = 0; q < 8; ++q) {
-    double e[8] = {0}, s2[8], y;
-    e[q] = 1.0;
-    cascade_d(e, 0.0, s2, &y);
-    for (int r = 0; r < 8; ++r) A[r * 8 + q] = s2[r];
-    C[q] = y;
-  }
-  Mat8 T(64, 0.0);
-  cd lam[4];
-  for (int j = 0; j < 4; ++j) {
-    const double a1 = kDecimSos[j][4], a2 = kDecimSos[j][5];
-    lam[j] = cd(-0.5 * a1, std::sqrt(a2 - 0.25 * a1 * a1));
-    cd v[8] = {};
-    const double p = A[(2 * j) * 8 + 2 * j], q = A[(2 * j) * 8 + 2 * j + 1];
-    v[2 * j] = q;
-    v[2 * j + 1] = lam[j] - p;
-    for (int k = j + 1; k < 4; ++k) {  // (A_kk - lambda) v_k = -sum_{l<k} A_kl v_l
-      cd r0 = 0, r1 = 0;
-      for (int l = 2 * j; l < 2 * k; ++l) {
-        r0 -= A[(2 * k) * 8 + l] * v[l];
-        r1 -= A[(2 * k + 1) * 8 + l] * v[l];
-      }
-      const cd m00 = A[(2 * k) * 8 + 2 * k] - lam[j], m01 = A[(2 * k) * 8 + 2 * k + 1];
-      const cd m10 = A[(2 * k + 1) * 8 + 2 * k], m11 = A[(2 * k + 1) * 8 + 2 * k + 1] - lam[j];
-      const cd det = m00 * m11 - m01 * m10;
-      v[2 * k] = (r0 * m11 - m01 * r1) / det;
-      v[2 * k + 1] = (m00 * r1 - m10 * r0) / det;
-    }
-    double nrm = 0;
-    int big = 0;
-    for (int i = 0; i < 8; ++i) {
-      nrm += std::norm(v[i]);
-      if (std::abs(v[i]) > std::abs(v[big])) big = i;
-    }
-    const cd rot = std::conj(v[big]) / std::abs(v[big]) / std::sqrt(nrm);
-    for (int i = 0; i < 8; ++i) {
-      const cd w = v[i] * rot;
-      T[i * 8 + 2 * j] = w.real();
-      T[i * 8 + 2 * j + 1] = w.imag();
-    }
-  }
-  Mat8 Ti;
-  mat_inverse8(T, Ti);
-  for (int i = 0; i < 64; ++i) X.ti[i / 8][i % 8] = (float)Ti[i];
-  for (int r = 0; r < 8; ++r) {  // T^-1 (zi), the steady state per unit input
-    double acc = 0;
-    for (int k = 0; k < 8; ++k) acc += Ti[r * 8 + k] * kDecimZi[k / 2][k % 2];
-    X.zim[r] = (float)acc;
-  }
-  Mat8 AtT = T;  // A^t T
-  for (int t = 0; t < kXtB; ++t) {
-    for (int q = 0; q < 8; ++q) {
-      double acc = 0;
-      for (int r = 0; r < 8; ++r) acc += C[r] * AtT[r * 8 + q];
-      X.cm[t][q] = (float)acc;
-    }
-    AtT = matmul8(A, AtT);
-  }
-  for (int j = 0; j < 4; ++j) {
-    const cd l16 = std::pow(lam[j], kXtB);
-    X.p16[j][0] = (float)l16.real();
-    X.p16[j][1] = (float)l16.imag();
-    for (int d = 0; d < kXtScan; ++d) {
-      const cd w = std::pow(lam[j], kXtB << d);
-      X.scan[d][j][0] = (float)w.real();
-      X.scan[d][j][1] = (float)w.imag();
-    }
-    for (int i = 0; i < 64; ++i) {
-      const cd w = std::pow(lam[j], kXtB * i);
-      X.lag[i][j][0] = (float)w.real();
-      X.lag[i][j][1] = (float)w.imag();
-    }
-  }
-}
-
-
 // ---- XA tables (xa_kernels.hip, tools/xa_proto.py): all-pole cascades in DF-I state
 // (y_k[t-1], y_k[t-2]) per section, real modal bases, the 25-tap FIR and frame-end forms ----
 struct ApD {
@@ -198,8 +99,12 @@ void ap_step_d(const ApD &c, const double in[8], double u, double out[8], double
   *y = x;
 }
 
-// Real modal basis of a cascade state matrix A (block lower triangular): mode j = the pole
-// pair of section j, eigenvector zero on sections < j, forward substitution below.
+// Real modal basis of a cascade state matrix A (block lower triangular: section k's state is
+// driven by the outputs of sections < k).  Mode j = the pole pair of section j, lambda_j =
+// sigma + i omega = (-a1 + i sqrt(4 a2 - a1^2)) / 2; its eigenvector v is zero on sections
+// < j, the null vector of (A_jj - lambda) on section j and found by forward substitution
+// below.  Columns (Re v, Im v) of T give T^-1 A T = diag([[sigma, omega], [-omega, sigma]]),
+// so a power of A is a per-mode complex power.
 void modal_basis(const Mat8 &A, const cd lam[4], Mat8 &T) {
   T.assign(64, 0.0);
   for (int j = 0; j < 4; ++j) {
@@ -446,7 +351,9 @@ struct zfft_plan {
   int K = 0;  // log2(zoom) decimation stages
   hipStream_t stream = nullptr;
   std::vector<float> user_window;
-  DevBuf lo, win, tw, in, yf, ping, pong, rows, ring, img, one_row, dec;
+  DevBuf lo, win, tw, in, in2, yf, ping, pong, rows, ring, img, one_row, dec;
+  hipStream_t copy_st = nullptr;            // H2D of the next batch in zfft_process
+  hipEvent_t h2d_ev[2] = {}, comp_ev[2] = {};
   int64_t lo_len = 0;
   int win_len = -1;
   double win_ss = 0.0;
@@ -460,10 +367,10 @@ struct zfft_plan {
   std::vector<std::string> mark_names;
   std::string names_buf;
   int n_marks = 0;
-  int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows, 3 exact tiles,
-                // 4 XA tiles (all-pole + FIR + half-rate all-pole)
+  int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows,
+                // 3 XA tiles (all-pole + FIR + half-rate all-pole)
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
-  DevBuf edge, xk, xt_tab, xa_tab, tws, means, z4;
+  DevBuf edge, xk, xa_tab, tws, means, z4;
   // waterfall rendering: colormap LUT (host copy + device), levels
   uint8_t lut[256 * 4] = {};
   bool lut_ready = false;         // lut holds the chosen map (built on first use)
@@ -471,6 +378,13 @@ struct zfft_plan {
   std::string cmap = "Default";
   double lev_lo = -220.0, lev_hi = -120.0;  // Waterfall.__init__ (S:1593-1598)
   DevBuf lut_d, rgba, al_hist, al_bins;
+  // Ordering across streams: every call that enqueues work first makes its stream wait for
+  // the plan's previous work (done_ev, recorded on done_st), then records done_ev after its
+  // own; the workspaces, tables and the ring are thus used in call order whatever streams the
+  // caller picks, and a synchronous table upload waits for done_ev first.
+  hipEvent_t done_ev = nullptr;
+  hipStream_t done_st = nullptr;
+  bool has_work = false;
 };
 
 namespace {
@@ -507,8 +421,14 @@ int choose_block(const zfft_plan *p, int64_t n, int ngroups) {
 
 int warmup(const zfft_plan *p) { return p->warm_override > 0 ? (p->warm_override + 15) & ~15 : 192; }
 
+int quiesce(zfft_plan *p);
+int use_stream(zfft_plan *p, hipStream_t st);
+int done_on(zfft_plan *p, hipStream_t st);
+
 int ensure_lo(zfft_plan *p, int64_t L) {
   if (p->lo_len >= L) return ZFFT_OK;
+  int rc = quiesce(p);
+  if (rc) return rc;
   int64_t cap = L;
   std::vector<float2> h(cap);
   const double r = p->cfg.f_lo / p->cfg.fs, sq2 = std::sqrt(2.0);
@@ -529,6 +449,8 @@ int ensure_lo(zfft_plan *p, int64_t L) {
 // welch builds get_window(window, nperseg); nperseg = min(N, L_d) (short-input branch).
 int ensure_window(zfft_plan *p, int nperseg) {
   if (p->win_len == nperseg) return ZFFT_OK;
+  int rc = quiesce(p);
+  if (rc) return rc;
   std::vector<double> w;
   if (p->cfg.window_kind == ZFFT_WIN_ARRAY) {
     if (nperseg != p->cfg.n_fft)
@@ -618,6 +540,9 @@ int64_t edge_window(int K) { return ((int64_t)1 << K) * (kEdge + 640); }
 constexpr int kXaMinFrames = 1024;
 constexpr int kXaMinFramesShort = 512;
 constexpr int64_t kXaShortFrame = (int64_t)1 << 19;
+// zfft_process pipelining: inputs of >= 64 MB go in batches of about 1 GB (at least two).
+constexpr size_t kPipeMinBytes = (size_t)64 << 20;
+constexpr size_t kPipeBatchBytes = (size_t)1 << 30;
 bool auto_xa(int frames, int64_t L) {
   return frames >= kXaMinFrames || (frames >= kXaMinFramesShort && L <= kXaShortFrame);
 }
@@ -717,27 +642,6 @@ int run_fused(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   return ZFFT_OK;
 }
 
-// Exact-tile path: one kernel per stage, one wave per frame, stage outputs natural layout.
-int run_xt(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t> &n,
-           const float2 **out, hipStream_t st) {
-  hipError_t e = p->ping.ensure((size_t)frames * n[1] * sizeof(float2));
-  if (e == hipSuccess && p->K > 1) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
-  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
-  const float2 *cur = nullptr;
-  for (int k = 0; k < p->K; ++k) {
-    float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
-    const InDesc src = k == 0 ? in : InDesc{cur, n[k], n[k], kInC64, 0};
-    e = launch_xt_stage(src, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
-                        p->xt_tab.as<XtModal>(), st);
-    if (e != hipSuccess) return hip_fail(e, "xt_stage launch");
-    mark(p, st, k == 0 ? "xt_stage_mix" : "xt_stage");
-    cur = dst;
-  }
-  *out = cur;
-  return ZFFT_OK;
-}
-
-
 // XA path: one kernel per stage, one wave per frame, stage outputs natural layout.
 int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t> &n,
            const float2 **out, hipStream_t st) {
@@ -764,9 +668,8 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  if (p->path == 4 || (p->path == 0 && auto_xa(frames, L)))
+  if (p->path == 3 || (p->path == 0 && auto_xa(frames, L)))
     return run_xa(p, in, frames, n, out, st);
-  if (p->path == 3) return run_xt(p, in, frames, n, out, st);
   if (use_fused(p, L)) return run_fused(p, in, L, frames, n, out, st);
   return run_exact(p, in, p->lo.as<float2>(), frames, n, out, st);
 }
@@ -774,11 +677,11 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
 // Real input at zoom 1 takes scipy.signal.welch's one-sided branch.
 bool onesided(const zfft_plan *p) { return p->cfg.in_dtype == kInF32R && p->K == 0; }
 
-// Valid entries per row: W, or in the one-sided case the length of the reference's slice
-// fftshift(P)[N/2 - W/2 : N/2 + W/2] of the N/2+1 one-sided bins.
+// Valid entries per row: the length of the reference's slice fftshift(P)[N//2 - W//2 :
+// N//2 + W//2] (S:2114): 2 (W//2), or in the one-sided case that slice of the N/2+1 bins.
 int row_length(const zfft_plan *p) {
   const int N = p->cfg.n_fft, W = p->cfg.n_win;
-  if (!onesided(p)) return W;
+  if (!onesided(p)) return W & ~1;  // [N/2 - W//2, N/2 + W//2): W - 1 entries for odd W
   const int a = N / 2 - W / 2, b = std::min(N / 2 + W / 2, N / 2 + 1);
   return std::max(0, b - a);
 }
@@ -858,8 +761,12 @@ int ensure_waterfall(zfft_plan *p) {
   if (e == hipSuccess) e = p->img.ensure((size_t)H * W * sizeof(float));
   if (e == hipSuccess) e = p->one_row.ensure((size_t)W * sizeof(float));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "waterfall allocation failed");
+  int rc = use_stream(p, p->stream);
+  if (rc) return rc;
   e = launch_waterfall_init(p->ring.as<float>(), H, W, p->stream);
   if (e != hipSuccess) return hip_fail(e, "waterfall init");
+  rc = done_on(p, p->stream);
+  if (rc) return rc;
   p->H = H;
   p->W = W;
   p->off = 0;
@@ -869,6 +776,30 @@ int ensure_waterfall(zfft_plan *p) {
 
 // A NULL stream handle means HIP's default (null) stream, as everywhere in HIP.
 hipStream_t pick_stream(zfft_plan *, void *s) { return (hipStream_t)s; }
+
+// Order `st` after everything the plan enqueued before (on any stream).
+int use_stream(zfft_plan *p, hipStream_t st) {
+  if (p->has_work && p->done_st != st) {
+    hipError_t e = hipStreamWaitEvent(st, p->done_ev, 0);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+  }
+  return ZFFT_OK;
+}
+// Mark the end of the plan's work enqueued so far on `st`.
+int done_on(zfft_plan *p, hipStream_t st) {
+  hipError_t e = hipEventRecord(p->done_ev, st);
+  if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+  p->done_st = st;
+  p->has_work = true;
+  return ZFFT_OK;
+}
+// Wait on the host until the plan's enqueued work is done (before a synchronous upload
+// overwrites a table that work may still read).
+int quiesce(zfft_plan *p) {
+  if (!p->has_work) return ZFFT_OK;
+  hipError_t e = hipEventSynchronize(p->done_ev);
+  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "hipEventSynchronize");
+}
 
 int enter(zfft_plan *p) {
   if (!p) return fail(ZFFT_EINVAL, "null plan");
@@ -903,8 +834,8 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
   if (!is_pow2(c.n_fft) || c.n_fft < 32 || c.n_fft > 65536)
     return fail(ZFFT_EINVAL, "n_fft must be a power of two in [32, 65536]");
   if (!is_pow2(c.zoom) || c.zoom > 512) return fail(ZFFT_EINVAL, "zoom must be 1, 2, 4, ..., 512");
-  if (c.n_win < 2 || c.n_win > c.n_fft || (c.n_win & 1))
-    return fail(ZFFT_EINVAL, "n_win must be even and in [2, n_fft]");
+  if (c.n_win < 2 || c.n_win > c.n_fft)
+    return fail(ZFFT_EINVAL, "n_win must be in [2, n_fft]");
   if (!(c.fs > 0) || !std::isfinite(c.fs) || !std::isfinite(c.f_lo))
     return fail(ZFFT_EINVAL, "fs must be positive and finite, f_lo finite");
   if (c.scroll != 1 && c.scroll != -1) return fail(ZFFT_EINVAL, "scroll must be +1 or -1");
@@ -928,9 +859,15 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
   if (c.window_kind == ZFFT_WIN_ARRAY)
     p->user_window.assign(window_or_null, window_or_null + c.n_fft);
   e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->copy_st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&p->done_ev, hipEventDisableTiming);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    e = hipEventCreateWithFlags(&p->h2d_ev[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->comp_ev[i], hipEventDisableTiming);
+  }
   if (e != hipSuccess) {
-    delete p;
-    return hip_fail(e, "hipStreamCreate");
+    zfft_plan_destroy(p);
+    return hip_fail(e, "hipStreamCreate / hipEventCreate");
   }
   // FFT twiddles tw[m] = exp(-2 pi i m / N), computed in fp64
   std::vector<float2> tw(c.n_fft);
@@ -949,18 +886,6 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
     e = p->tws.ensure(ts.size() * sizeof(float2));
     if (e == hipSuccess)
       e = hipMemcpy(p->tws.p, ts.data(), ts.size() * sizeof(float2), hipMemcpyHostToDevice);
-  }
-  if (e == hipSuccess) {
-    XtModal xt;
-    xt_build_tables(xt);
-    xt.sos = sos32();
-    for (int t = 0; t < kXtB; ++t) {  // LO step across a sub-block (lo[n] = sqrt2 w^n)
-      const double ph = -2.0 * M_PI * std::fmod((double)t * c.f_lo / c.fs, 1.0);
-      xt.wt[t][0] = (float)std::cos(ph);
-      xt.wt[t][1] = (float)std::sin(ph);
-    }
-    e = p->xt_tab.ensure(sizeof(XtModal));
-    if (e == hipSuccess) e = hipMemcpy(p->xt_tab.p, &xt, sizeof(XtModal), hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) {
     static XaTab xa{};
@@ -983,12 +908,19 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
 int zfft_plan_destroy(zfft_plan *p) {
   if (!p) return ZFFT_OK;
   (void)hipSetDevice(p->cfg.device);
+  if (p->has_work) (void)hipEventSynchronize(p->done_ev);
   if (p->stream) (void)hipStreamSynchronize(p->stream);
-  for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->yf, &p->ping, &p->pong, &p->rows,
-                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xt_tab, &p->xa_tab,
+  for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->in2, &p->yf, &p->ping, &p->pong, &p->rows,
+                    &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
                     &p->tws, &p->means, &p->z4})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
+  if (p->done_ev) (void)hipEventDestroy(p->done_ev);
+  for (int i = 0; i < 2; ++i) {
+    if (p->h2d_ev[i]) (void)hipEventDestroy(p->h2d_ev[i]);
+    if (p->comp_ev[i]) (void)hipEventDestroy(p->comp_ev[i]);
+  }
+  if (p->copy_st) (void)hipStreamSynchronize(p->copy_st), (void)hipStreamDestroy(p->copy_st);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
   return ZFFT_OK;
@@ -1021,9 +953,8 @@ int zfft_plan_timing(zfft_plan *p, int32_t enable) {
 }
 
 int zfft_plan_path(zfft_plan *p, int32_t path) {
-  if (!p || path < 0 || path > 4)
-    return fail(ZFFT_EINVAL,
-                "path must be 0 (auto), 1 (exact), 2 (fused), 3 (exact tiles) or 4 (XA tiles)");
+  if (!p || path < 0 || path > 3)
+    return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused) or 3 (XA tiles)");
   p->path = path;
   return ZFFT_OK;
 }
@@ -1074,7 +1005,12 @@ int zfft_process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frame
   int rc = enter(p);
   if (rc) return rc;
   if (!d_iq || !d_rows) return fail(ZFFT_EINVAL, "null device pointer");
-  return process_device(p, d_iq, L, frames, d_rows, pick_stream(p, hip_stream));
+  hipStream_t st = pick_stream(p, hip_stream);
+  rc = use_stream(p, st);
+  if (rc) return rc;
+  rc = process_device(p, d_iq, L, frames, d_rows, st);
+  if (rc) return rc;
+  return done_on(p, st);
 }
 
 int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float *rows_out) {
@@ -1082,19 +1018,50 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
   if (rc) return rc;
   if (!iq || !rows_out) return fail(ZFFT_EINVAL, "null host pointer");
   if (L < 1 || frames < 1) return fail(ZFFT_EINVAL, "n_samples and n_frames must be >= 1");
-  const size_t in_bytes = (size_t)frames * L * in_elem_bytes(p->cfg.in_dtype);
+  const size_t frame_bytes = (size_t)L * in_elem_bytes(p->cfg.in_dtype);
   const size_t row_bytes = (size_t)frames * p->cfg.n_win * sizeof(float);
-  hipError_t e = p->in.ensure(in_bytes);
+  // Batches: one for a small call; otherwise >= 2 so that the H2D copy of batch k+1 (copy
+  // stream) runs while batch k is computed (plan stream).  From pinned memory both are
+  // asynchronous; from pageable memory HIP stages the copy on this thread, which then copies
+  // batch k+1 while the GPU computes batch k.  Batches keep >= kXaMinFrames frames when the
+  // call has twice that, so the schedule is the one a device call of that size gets.
+  int B = frames;
+  const size_t total = (size_t)frames * frame_bytes;
+  if (total >= kPipeMinBytes && frames >= 2) {
+    int nb = std::max<int64_t>(2, (int64_t)((total + kPipeBatchBytes - 1) / kPipeBatchBytes));
+    B = (frames + nb - 1) / nb;
+    if (frames >= 2 * kXaMinFrames) B = std::max(B, kXaMinFrames);
+  }
+  const int nb = (frames + B - 1) / B;
+  hipError_t e = p->in.ensure((size_t)B * frame_bytes);
+  if (e == hipSuccess && nb > 1) e = p->in2.ensure((size_t)B * frame_bytes);
   if (e == hipSuccess) e = p->rows.ensure(row_bytes);
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "staging allocation failed");
-  e = hipMemcpyAsync(p->in.p, iq, in_bytes, hipMemcpyHostToDevice, p->stream);
-  if (e != hipSuccess) return hip_fail(e, "H2D copy");
-  rc = process_device(p, p->in.p, L, frames, p->rows.as<float>(), p->stream);
+  rc = use_stream(p, p->stream);
+  if (rc == ZFFT_OK && nb > 1) rc = use_stream(p, p->copy_st);
   if (rc) return rc;
+  const char *src = (const char *)iq;
+  for (int k = 0; k < nb; ++k) {
+    const int f0 = k * B, nk = std::min(B, frames - f0), buf = k & 1;
+    void *dst = buf ? p->in2.p : p->in.p;
+    hipStream_t cs = nb > 1 ? p->copy_st : p->stream;
+    if (k >= 2) e = hipStreamWaitEvent(cs, p->comp_ev[buf], 0);  // batch k-2 done with dst
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, src + (size_t)f0 * frame_bytes, (size_t)nk * frame_bytes,
+                                            hipMemcpyHostToDevice, cs);
+    if (e == hipSuccess && nb > 1) e = hipEventRecord(p->h2d_ev[buf], cs);
+    if (e == hipSuccess && nb > 1) e = hipStreamWaitEvent(p->stream, p->h2d_ev[buf], 0);
+    if (e != hipSuccess) return hip_fail(e, "H2D copy");
+    rc = process_device(p, dst, L, nk, p->rows.as<float>() + (int64_t)f0 * p->cfg.n_win, p->stream);
+    if (rc) return rc;
+    if (nb > 1 && (e = hipEventRecord(p->comp_ev[buf], p->stream)) != hipSuccess)
+      return hip_fail(e, "event record");
+  }
   e = hipMemcpyAsync(rows_out, p->rows.p, row_bytes, hipMemcpyDeviceToHost, p->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
-  if (e != hipSuccess) return hip_fail(e, "D2H copy / sync");
-  return ZFFT_OK;
+  if (e != hipSuccess) return hip_fail(e, "D2H copy");
+  rc = done_on(p, p->stream);
+  if (rc) return rc;
+  e = hipStreamSynchronize(p->stream);
+  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "sync");
 }
 
 int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t *out_len) {
@@ -1105,14 +1072,16 @@ int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t
   rc = check_lengths(p, L, 1, n);
   if (rc) return rc;
   const size_t in_bytes = (size_t)L * in_elem_bytes(p->cfg.in_dtype);
+  rc = ensure_lo(p, L);  // (a table upload waits for the plan's earlier work)
+  if (rc) return rc;
   hipError_t e = p->in.ensure(in_bytes);
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "staging allocation failed");
+  rc = use_stream(p, p->stream);
+  if (rc) return rc;
   e = hipMemcpyAsync(p->in.p, iq, in_bytes, hipMemcpyHostToDevice, p->stream);
   if (e != hipSuccess) return hip_fail(e, "H2D copy");
   const float2 *x;
   if (p->K == 0) {  // zoomfft(x, 1) still mixes (S:2093-2094)
-    rc = ensure_lo(p, L);
-    if (rc) return rc;
     e = p->dec.ensure((size_t)L * sizeof(float2));
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "allocation failed");
     e = launch_ingest(input_of(p, p->in.p, L), p->lo.as<float2>(), p->dec.as<float2>(), 1,
@@ -1125,8 +1094,11 @@ int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t
   }
   const int64_t m = n[p->K];
   e = hipMemcpyAsync(out_iq, x, (size_t)m * sizeof(float2), hipMemcpyDeviceToHost, p->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
-  if (e != hipSuccess) return hip_fail(e, "D2H copy / sync");
+  if (e != hipSuccess) return hip_fail(e, "D2H copy");
+  rc = done_on(p, p->stream);
+  if (rc) return rc;
+  e = hipStreamSynchronize(p->stream);
+  if (e != hipSuccess) return hip_fail(e, "sync");
   if (out_len) *out_len = m;
   return ZFFT_OK;
 }
@@ -1155,15 +1127,13 @@ int zfft_waterfall_push_device(zfft_plan *p, const float *d_rows, int32_t count,
   rc = ensure_waterfall(p);
   if (rc) return rc;
   hipStream_t st = pick_stream(p, hip_stream);
-  if (st != p->stream) {  // ring init was enqueued on the plan stream
-    hipError_t e = hipStreamSynchronize(p->stream);
-    if (e != hipSuccess) return hip_fail(e, "sync");
-  }
+  rc = use_stream(p, st);  // after the ring init and the rows' producer, on any stream
+  if (rc) return rc;
   hipError_t e = launch_waterfall_push(p->ring.as<float>(), p->H, p->W, d_rows, p->W, count,
                                        p->off, p->cfg.scroll, st);
   if (e != hipSuccess) return hip_fail(e, "waterfall push");
   p->off = ((p->off + (int64_t)count * p->cfg.scroll) % p->H + p->H) % p->H;
-  return ZFFT_OK;
+  return done_on(p, st);
 }
 
 int zfft_waterfall_push(zfft_plan *p, const float *row) {
@@ -1173,6 +1143,8 @@ int zfft_waterfall_push(zfft_plan *p, const float *row) {
   if (rc) return rc;
   const float *src = p->last_row;
   if (row) {
+    rc = use_stream(p, p->stream);  // one_row may still be read by the previous push
+    if (rc) return rc;
     hipError_t e = hipMemcpyAsync(p->one_row.p, row, (size_t)p->W * sizeof(float),
                                   hipMemcpyHostToDevice, p->stream);
     if (e != hipSuccess) return hip_fail(e, "H2D row");
@@ -1191,11 +1163,14 @@ int zfft_waterfall_read(zfft_plan *p, float *img_out) {
   if (!img_out) return fail(ZFFT_EINVAL, "null output");
   rc = ensure_waterfall(p);
   if (rc) return rc;
+  rc = use_stream(p, p->stream);
+  if (rc) return rc;
   hipError_t e = launch_waterfall_read(p->ring.as<float>(), p->H, p->W, p->off, p->img.as<float>(),
                                        p->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(img_out, p->img.p, (size_t)p->H * p->W * sizeof(float),
                        hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = done_on(p, p->stream) == ZFFT_OK ? hipSuccess : hipErrorUnknown;
   if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
   return e == hipSuccess ? ZFFT_OK : hip_fail(e, "waterfall read");
 }
@@ -1241,16 +1216,14 @@ int zfft_waterfall_render_device(zfft_plan *p, uint8_t *d_rgba, void *hip_stream
     build_lut(p->cmap.c_str(), p->lut);
     p->lut_ready = true;
   }
+  hipStream_t st = pick_stream(p, hip_stream);
+  rc = use_stream(p, st);
+  if (rc) return rc;
   if (!p->lut_uploaded) {
     e = p->lut_d.ensure(sizeof(p->lut));
-    if (e == hipSuccess) e = hipMemcpyAsync(p->lut_d.p, p->lut, sizeof(p->lut), hipMemcpyHostToDevice, p->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(p->lut_d.p, p->lut, sizeof(p->lut), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return hip_fail(e, "LUT upload");
     p->lut_uploaded = true;
-  }
-  hipStream_t st = pick_stream(p, hip_stream);
-  if (st != p->stream) {  // ring init / LUT upload were enqueued on the plan stream
-    e = hipStreamSynchronize(p->stream);
-    if (e != hipSuccess) return hip_fail(e, "sync");
   }
   // makeARGB levels (pyqtgraph functions.py): equal levels -> max = nextafter(max, 2 max);
   // scale = lut size / (max - min) (1 when the range is 0)
@@ -1260,7 +1233,8 @@ int zfft_waterfall_render_device(zfft_plan *p, uint8_t *d_rgba, void *hip_stream
   if (rng == 0.0) rng = 1.0;
   e = launch_waterfall_render(p->ring.as<float>(), p->H, p->W, p->off, p->lut_d.p, lo, 256.0 / rng,
                               d_rgba, st);
-  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "waterfall render");
+  if (e != hipSuccess) return hip_fail(e, "waterfall render");
+  return done_on(p, st);
 }
 
 int zfft_waterfall_render(zfft_plan *p, uint8_t *rgba_out) {
@@ -1275,6 +1249,7 @@ int zfft_waterfall_render(zfft_plan *p, uint8_t *rgba_out) {
   rc = zfft_waterfall_render_device(p, p->rgba.as<uint8_t>(), p->stream);
   if (rc) return rc;
   e = hipMemcpyAsync(rgba_out, p->rgba.p, bytes, hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = done_on(p, p->stream) == ZFFT_OK ? hipSuccess : hipErrorUnknown;
   if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
   return e == hipSuccess ? ZFFT_OK : hip_fail(e, "render copy");
 }
@@ -1290,6 +1265,8 @@ int zfft_waterfall_autolevel(zfft_plan *p, double *minlev, double *maxlev) {
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "autolevel workspace allocation failed");
   // pass 1: counts per top-16-bit key of the pixels < 0
   std::vector<unsigned> h1(65536);
+  rc = use_stream(p, p->stream);
+  if (rc) return rc;
   e = hipMemsetAsync(p->al_hist.p, 0, 65536 * sizeof(unsigned), p->stream);
   if (e == hipSuccess) e = launch_autolevel_hist_hi(p->ring.as<float>(), n, p->al_hist.as<unsigned>(), p->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(h1.data(), p->al_hist.p, 65536 * sizeof(unsigned), hipMemcpyDeviceToHost, p->stream);
@@ -1333,6 +1310,7 @@ int zfft_waterfall_autolevel(zfft_plan *p, double *minlev, double *maxlev) {
   if (e == hipSuccess)
     e = launch_autolevel_hist_lo(p->ring.as<float>(), n, p->al_bins.as<unsigned>(), nb, p->al_hist.as<unsigned>(), p->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(h2.data(), p->al_hist.p, (size_t)nb * 65536 * sizeof(unsigned), hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = done_on(p, p->stream) == ZFFT_OK ? hipSuccess : hipErrorUnknown;
   if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
   if (e != hipSuccess) return hip_fail(e, "autolevel pass 2");
   double val[4];

@@ -66,7 +66,8 @@ int zfft_ring_create(int64_t chunk_size, int32_t in_dtype, zfft_ring **out) {
   *out = nullptr;
   if (chunk_size < 1 || chunk_size > ((int64_t)1 << 26))
     return zfft::set_error("chunk_size must be in [1, 2^26]"), ZFFT_EINVAL;
-  if (in_dtype < 0 || in_dtype > 2) return zfft::set_error("in_dtype must be 0, 1 or 2"), ZFFT_EINVAL;
+  if (in_dtype < 0 || in_dtype > 3)  // 3: real float32 (Data.new_real, T:1413-1417)
+    return zfft::set_error("in_dtype must be 0, 1, 2 or 3"), ZFFT_EINVAL;
   zfft_ring *r = new zfft_ring;
   r->chunk_size = chunk_size;
   r->max_size = 16 * chunk_size;
@@ -93,9 +94,14 @@ int zfft_ring_destroy(zfft_ring *r) {
 
 int zfft_ring_add(zfft_ring *r, const void *chunk, int64_t n) {
   if (!r || (!chunk && n > 0)) return zfft::set_error("null argument"), ZFFT_EINVAL;
-  if (n < 0 || n > r->max_size)  // a longer chunk fails the reference's slice assignment
-    return zfft::set_error("chunk longer than the ring (max_size = 16 * chunk_size)"), ZFFT_EINVAL;
+  if (n < 0) return zfft::set_error("negative chunk length"), ZFFT_EINVAL;
   std::lock_guard<std::mutex> g(r->mu);
+  if (n > r->max_size) {
+    // the reference folds back (size = 0, T:1439-1442) and then fails the slice assignment
+    // data[0:n] = chunk (T:1447) with a ValueError: nothing is written or counted
+    r->size = 0;
+    return zfft::set_error("chunk longer than the ring (max_size = 16 * chunk_size)"), ZFFT_EINVAL;
+  }
   int64_t new_size = r->size + n;
   if (new_size > r->max_size) {  // fold back: overwrite from the start (T:1437-1442)
     r->size = 0;

@@ -113,8 +113,9 @@ class ZoomFFT:
         return [n for n in raw.decode().split(",") if n]
 
     def set_path(self, path: int) -> None:
-        """0 auto, 1 exact reference pass order, 2 fused interior + exact edges, 3 DF2T exact
-        tiles, 4 XA tiles (all-pole + FIR + half-rate all-pole; the auto choice for >= 1024 frames, or >= 512 frames of <= 2^19 samples)."""
+        """0 auto, 1 exact reference pass order (blocked), 2 fused interior + exact edges
+        (blocked), 3 XA tiles (all-pole + FIR + half-rate all-pole, one wave per frame; the
+        auto choice for >= 1024 frames, or >= 512 frames of <= 2^19 samples)."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
 
     def set_welch(self, mode: int) -> None:
@@ -163,6 +164,13 @@ class ZoomFFT:
         if n != self.n_win:  # one-sided rows (real input at zoom 1)
             out = np.ascontiguousarray(out[:, :n])
         return out[0] if single else out
+
+    def process_host(self, iq_ptr: int, n_samples: int, n_frames: int, rows_ptr: int) -> None:
+        """zfft_process on raw host pointers (e.g. a pinned torch tensor's data_ptr()): frames in
+        the plan's input format, rows n_frames * n_win floats.  Synchronous; large inputs go in
+        batches whose H2D copy overlaps the previous batch's compute."""
+        check(self.lib.zfft_process(self._plan, ctypes.c_void_p(iq_ptr), int(n_samples),
+                                    int(n_frames), ctypes.c_void_p(rows_ptr)), "zfft_process")
 
     def process_device(self, d_iq_ptr: int, n_samples: int, n_frames: int, d_rows_ptr: int,
                        stream: int = 0) -> None:
@@ -213,7 +221,9 @@ class ZoomFFT:
         return img
 
     def waterfall_reset(self, scroll: int) -> None:
+        """Waterfall.init_image with a (possibly new) scroll direction (S:1625-1636, 2074-2077)."""
         check(self.lib.zfft_waterfall_reset(self._plan, int(scroll)), "zfft_waterfall_reset")
+        self.scroll = int(scroll)
 
     # ---------------------------------------------------------------- rendering (§8f-2)
     def waterfall_colormap(self, name: str) -> None:
@@ -247,10 +257,10 @@ class ZoomFFT:
         return out
 
     def waterfall_render_device(self, d_rgba_ptr: int, stream: int = 0) -> None:
+        """RGBA8 pixels of the ring into device memory (H*W*4 bytes), enqueued on `stream`."""
         check(self.lib.zfft_waterfall_render_device(self._plan, ctypes.c_void_p(d_rgba_ptr),
-                                                    ctypes.c_void_p(stream)),
+                                                    ctypes.c_void_p(stream or None)),
               "zfft_waterfall_render_device")
-        self.scroll = int(scroll)
 
 
 _IN_DTYPES = {"complex64": (0, np.complex64, 1), "complex32": (1, np.float16, 2),

@@ -185,38 +185,52 @@ class Data:
     worker's `get_data_start(); size = real_size; chunk = data[:size]; get_data_end()`
     (T:1516-1520).  `get_data_start` drains the ring, so `data[:real_size]` stays intact
     while the reader keeps adding (the reference hands out a view it keeps overwriting).
-    `in_dtype="cu8"` takes the RTL-SDR's raw interleaved uint8 I,Q bytes.  The NewtRap
-    pacing (`delay_time`) is out of scope; `target` is kept as a plain attribute."""
+    `new_complex` takes complex64 (or, with `in_dtype="cu8"`, the RTL-SDR's raw interleaved
+    uint8 I,Q bytes), `new_real` real float32 samples (AudioPan).  `fft_size` stands for
+    AppState.fft_size, the target setter's lower bound (T:1477).  The NewtRap pacing
+    (`delay_time`, the sleep in add) is out of scope; `target` keeps the reference's rules.
+    Pinned by tests/golden/ring.npz, sequences of the reference's own class."""
 
-    def __init__(self, chunk_size: int = 8196 * 2, in_dtype: str = "complex64"):
+    def __init__(self, chunk_size: int = 8196 * 2, in_dtype: str = "complex64",
+                 fft_size: int = 2048):
         self.chunk_size = int(chunk_size)
-        self.max_size = self.chunk_size * 16
-        self.target_size = self.max_size * .9
+        self.max_size = self.chunk_size * 16          # T:1406
+        self.target_size = self.max_size * .9         # T:1407
         self.in_dtype = in_dtype
+        self.fft_size = int(fft_size)
         self._ring = None
         self.data = None
+        self.real = False
         self.real_size = 0
         self.total_size = 0
 
-    def new_complex(self):
+    def _new(self, in_dtype: str, real: bool):
         from .engine import IQRing
         if self._ring is not None:
             self._ring.close()
-        self._ring = IQRing(self.chunk_size, self.in_dtype)
-        self.real = False
+        self._ring = IQRing(self.chunk_size, in_dtype)
+        self.real = real
         self.data, self.real_size, self.total_size = None, 0, 0
         return self
 
+    def new_complex(self):
+        """T:1419-1423 (new_common: empty buffer, counts 0)."""
+        return self._new("complex64" if self.in_dtype == "f32" else self.in_dtype, False)
+
     def new_real(self):
-        raise NotImplementedError("real (AudioPan) input is SURVEY §8f-4, not built yet")
+        """T:1413-1417: real samples (AudioPan's float32 stream)."""
+        return self._new("f32", True)
 
     def add(self, chunk):
+        """T:1433-1457 without the pacing sleep: fold back at max_size, then the target clip
+        np.clip(target_size, 8192, max_size) (T:1445) before the write."""
+        self.target_size = np.clip(self.target_size, 8192, self.max_size)
         self._ring.add(chunk)
 
     def get_data_start(self):
         frame, total = self._ring.take()
         self.data = frame
-        self.real_size = len(frame) if self.in_dtype in ("complex64", "f32") else len(frame) // 2
+        self.real_size = len(frame) if self._ring.in_dtype in ("complex64", "f32") else len(frame) // 2
         self.total_size = total
 
     def get_data_end(self):
@@ -227,12 +241,17 @@ class Data:
         return self._ring.process(plan)
 
     @property
+    def size(self):
+        """Data.size: where the next chunk goes (T:1426, 1449)."""
+        return self._ring.state()[0]
+
+    @property
     def target(self):
         return self.target_size
 
     @target.setter
     def target(self, t):
-        if t <= self.max_size:
+        if t >= self.fft_size and t <= self.max_size:  # T:1474-1479
             self.target_size = t
 
     @property

@@ -36,7 +36,7 @@ def test_golden_rows(c):
     assert_row_close(row, golden_rows()[c["name"]], c["name"])
 
 
-@pytest.mark.parametrize("path", [1, 3, 4])
+@pytest.mark.parametrize("path", [1, 3])
 def test_golden_rows_every_schedule(path):
     """Every decimator schedule reproduces the reference rows (zoom > 1 cases)."""
     for c in CASES:
@@ -249,15 +249,15 @@ def test_fused_interior_matches_exact_pipeline(oracle_lib, N, z, L):
     from pypanadapter_amd import ZoomFFT
     x = _frames(2, L, N, z, N // z, seed0=4200)
     out = {}
-    for path in (1, 2, 3, 4):
+    for path in (1, 2, 3):
         with ZoomFFT(N, z, 2.4e6) as plan:
             plan.set_path(path)
             out[path] = (plan.rows(x), plan.decimate(x[0]))
     ref_dec = oracle_lib.zoomfft(x[0], z, 2.4e6)
     # fp32 relative error of the decimated IQ vs float64: DF2T schedules ~1e-6 per stage;
     # XA (all-pole + FIR + half-rate all-pole, tools/xa_proto.py) ~8e-6 per stage
-    tol = {1: 3e-6, 2: 3e-6, 3: 3e-6, 4: 1e-5 * np.log2(z)}
-    for path in (1, 2, 3, 4):
+    tol = {1: 3e-6, 2: 3e-6, 3: 1e-5 * np.log2(z)}
+    for path in (1, 2, 3):
         d = out[path][1]
         assert d.shape == ref_dec.shape
         err = np.abs(d - ref_dec) / np.abs(ref_dec).max()
@@ -266,8 +266,7 @@ def test_fused_interior_matches_exact_pipeline(oracle_lib, N, z, L):
         ref = oracle_lib.psd_row(x[f], 2.4e6, N, z, N // z)
         assert_row_close(out[1][0][f], ref, "exact")
         assert_row_close(out[2][0][f], ref, "fused")
-        assert_row_close(out[3][0][f], ref, "exact tiles")
-        assert_row_close(out[4][0][f], ref, "XA tiles")
+        assert_row_close(out[3][0][f], ref, "XA tiles")
 
 
 def test_size_independent_properties():

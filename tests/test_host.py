@@ -46,7 +46,7 @@ def _cfg(**kw):
 
 
 @pytest.mark.parametrize("bad", [dict(n_fft=1000), dict(n_fft=16), dict(zoom=3), dict(zoom=1024),
-                                 dict(n_win=513), dict(n_win=8192), dict(n_win=0), dict(fs=0.0),
+                                 dict(n_win=1), dict(n_win=8192), dict(n_win=0), dict(fs=0.0),
                                  dict(scroll=0), dict(window_kind=99), dict(window_kind=100),
                                  dict(in_dtype=4), dict(in_dtype=-1), dict(flip_input=2)])
 def test_config_validation(zfft_lib, bad):

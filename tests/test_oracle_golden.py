@@ -94,3 +94,16 @@ def test_waterfall_sequences(impl, oracle_lib):
             if (k + 1) in m["snaps"]:
                 np.testing.assert_array_equal(w.img_array.astype(np.float32),
                                               wf[f"{m['name']}/img{k + 1}"], err_msg=m["name"])
+
+
+def test_oracle_odd_width_is_the_reference_slice(oracle_lib):
+    """fftshift(P)[N//2 - W//2 : N//2 + W//2] for odd W has W - 1 entries (S:2114); the C
+    oracle and the library-call restatement agree on it."""
+    from oracle import scipy_path
+    from pypanadapter_amd import synth
+    x = synth.make_iq(32768, 2.4e6, 5, n_fft=1024, zoom=4, n_win=256)
+    for W in (255, 97, 1024):
+        a = oracle_lib.psd_row(x, 2.4e6, 1024, 4, W)
+        b = scipy_path.psd_row(x, 2.4e6, 1024, 4, W)
+        assert a.shape == b.shape == (W & ~1,)
+        np.testing.assert_allclose(a, b, atol=1e-7)

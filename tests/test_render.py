@@ -99,3 +99,28 @@ def test_waterfall_facade_rendering():
     np.testing.assert_array_equal(wf.render(), rr.render(wf.img_array, rr.lookup_table("Tropical"), lv))
     wf.lookuptable("nope")
     np.testing.assert_array_equal(wf.render(), rr.render(wf.img_array, rr.lookup_table("Default"), lv))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("side_stream", [False, True])
+def test_render_device_matches_host_render(side_stream):
+    """zfft_waterfall_render_device (into a device buffer, on a caller stream) gives the
+    same pixels as the host-buffer render; the plan's scroll survives a reset."""
+    import torch
+    plan = _filled_plan(W=256, seed=11, rows=50)
+    try:
+        plan.waterfall_colormap("Tropical")
+        want = plan.waterfall_render()
+        d = torch.zeros(want.size, dtype=torch.uint8, device="cuda")
+        st = torch.cuda.Stream() if side_stream else torch.cuda.current_stream()
+        with torch.cuda.stream(st):
+            plan.waterfall_render_device(d.data_ptr(), st.cuda_stream)
+        st.synchronize()
+        np.testing.assert_array_equal(d.cpu().numpy().reshape(want.shape), want)
+        plan.waterfall_reset(-1)
+        assert plan.scroll == -1
+        plan.waterfall_push((-170 + np.zeros(256)).astype(np.float32))
+        img = plan.waterfall_image()
+        assert img.shape == (64, 256) and np.all(img[:-1] <= 0)
+    finally:
+        plan.close()

@@ -62,3 +62,34 @@ def test_gloo_two_ranks_match_single_process(tmp_path, n_frames):
     got = np.load(out)
     ref = np.stack([coracle.psd_row(f, 2.4e6, 256, 4, 64) for f in frames]).astype(np.float32)
     np.testing.assert_array_equal(got, ref)
+
+
+def _gpu_worker(rank, world, port, frames, path, out_path):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pypanadapter_amd import ZoomFFT
+    with ZoomFFT(1024, 8, 2.4e6) as plan:  # both ranks on device 0 (the GPU box has one)
+        plan.set_path(path)
+        rows = run_sharded(frames, plan.rows, rank, world, dist=dist)
+    if rank == 0:
+        np.save(out_path, rows)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", [0, 3])
+def test_hip_two_ranks_bit_equal_single_process(tmp_path, path):
+    """rows of frames sharded over two rank processes (HIP plans, gloo
+    gather) equal the single-process rows bit for bit."""
+    from pypanadapter_amd import ZoomFFT, synth
+    frames = np.stack([synth.make_iq(65536, 2.4e6, 300 + f, n_fft=1024, zoom=8, n_win=128)
+                       for f in range(7)])
+    with ZoomFFT(1024, 8, 2.4e6) as plan:
+        plan.set_path(path)
+        ref = plan.rows(frames)
+    out = str(tmp_path / "rows.npy")
+    mp.spawn(_gpu_worker, args=(2, _free_port(), frames, path, out), nprocs=2, join=True)
+    np.testing.assert_array_equal(np.load(out), ref)

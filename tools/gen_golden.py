@@ -11,10 +11,12 @@ and exits quietly without it.  It loads the reference scripts unmodified through
   * `PSD.update(fake_self)`                        pypanadapter_thread.py:1513-1549
   * `Waterfall.image_update(psd)`                  pypanadapter_spectrum.py:1638-1664
   * `ApplicationDisplay.zoomfft(fake_self, x, r)`  pypanadapter_spectrum.py:2088-2100
+  * `Data` (new_complex / new_real / add / get_data_start / data[:real_size] /
+    get_data_end / target)                      pypanadapter_thread.py:1400-1483, 1516-1520
 
 Outputs (all data, no reference source): tests/golden/cases.json (metadata, input
 digests), rows.npz (float64 rows), inputs.npz (small stored complex64 inputs),
-zoomfft.npz (decimated IQ), waterfall.npz (image snapshots).
+zoomfft.npz (decimated IQ), waterfall.npz (image snapshots), ring.npz (Data sequences).
 
 Run:  python tools/gen_golden.py
 """
@@ -214,6 +216,81 @@ def waterfall_sequences(S):
     return seqs, meta
 
 
+def ring_sequences(T):
+    """T's own `Data` ring (T:1400-1483) driven by seeded add / drain / target sequences.
+
+    `Data.add` sleeps `delay_time` (the NewtRap pacing, T:1455-1457): the loaded module's
+    `time` is replaced by one whose sleep returns at once (the module namespace, not the
+    reference source).  A drain is the PSD worker's T:1516-1520: get_data_start(); size =
+    real_size; chunk = data[:size]; get_data_end().  Recorded per step: the op, its input,
+    (size, real_size, total_size, target_size) after it, and every drained frame."""
+    import contextlib
+    import io
+    import time
+    import types
+    T.time = types.SimpleNamespace(sleep=lambda s: None, monotonic=time.monotonic)
+    T.AppState.fft_size = 1024  # the target setter's lower bound (T:1477)
+    out, meta = {}, []
+
+    def run(name, chunk, real, n_ops, seed, p_add=0.75, p_target=0.08, max_len=3):
+        rng = np.random.default_rng(seed)
+        d = T.Data(chunk)
+        (d.new_real if real else d.new_complex)()
+        ops, states, lens, targets = [], [], [], []
+        n_drain = 0
+        for i in range(n_ops):
+            u = rng.random()
+            if u < p_target:
+                t = float(rng.choice([100.0, 1023.0, 1024.0, 5000.0, 9000.0, 16.0 * chunk,
+                                      16.0 * chunk + 1.0, 40000.0]))
+                d.target = t
+                ops.append(2)
+                targets.append(t)
+                lens.append(0)
+            elif u < p_target + p_add:
+                n = int(rng.integers(0, max_len * chunk + 1))
+                if real:
+                    x = rng.standard_normal(n).astype(np.float32)
+                else:
+                    x = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+                out[f"{name}/in{i}"] = x
+                if n > d.max_size:
+                    with contextlib.suppress(ValueError):  # numpy refuses the slice assignment
+                        d.add(x)
+                    ops.append(3)
+                else:
+                    d.add(x)
+                    ops.append(0)
+                lens.append(n)
+                targets.append(0.0)
+            else:
+                with contextlib.redirect_stdout(io.StringIO()):  # get_data_end prints delay_time
+                    d.get_data_start()
+                    size = d.real_size
+                    frame = np.array(d.data[:size])
+                    total = d.total_size
+                    d.get_data_end()
+                out[f"{name}/frame{i}"] = frame.astype(np.float32 if real else np.complex64)
+                out[f"{name}/frame_total{i}"] = np.array([total], np.int64)
+                ops.append(1)
+                lens.append(size)
+                targets.append(0.0)
+                n_drain += 1
+            states.append([d.size, d.real_size, d.total_size, float(d.target_size)])
+        out[f"{name}/ops"] = np.array(ops, np.int8)
+        out[f"{name}/lens"] = np.array(lens, np.int64)
+        out[f"{name}/targets"] = np.array(targets, np.float64)
+        out[f"{name}/states"] = np.array(states, np.float64)
+        meta.append(dict(name=name, chunk_size=chunk, real=real, n_ops=n_ops, seed=seed,
+                         drains=n_drain, fft_size=1024, max_size=16 * chunk))
+
+    run("c64", 64, False, 300, 1)
+    run("c520", 520, False, 160, 2, max_len=1)       # target_size clip: 16*520 = 8320 > 8192
+    run("real64", 64, True, 200, 3)                  # new_real (T:1413-1417)
+    run("c64_overlong", 64, False, 80, 4, max_len=20)  # chunks past max_size raise
+    return out, meta
+
+
 def main():
     if not os.path.isdir("/root/reference"):
         print("gen_golden: /root/reference absent, nothing to do")
@@ -266,16 +343,18 @@ def main():
         zf[name + "/meta"] = np.array([n_fft, n_avg, ratio, seed], dtype=np.int64)
 
     wf, wf_meta = waterfall_sequences(S)
+    ring, ring_meta = ring_sequences(T)
 
     np.savez_compressed(os.path.join(OUT, "rows.npz"), **rows)
     np.savez_compressed(os.path.join(OUT, "inputs.npz"), **inputs)
     np.savez_compressed(os.path.join(OUT, "zoomfft.npz"), **zf)
     np.savez_compressed(os.path.join(OUT, "waterfall.npz"), **wf)
+    np.savez_compressed(os.path.join(OUT, "ring.npz"), **ring)
     with open(os.path.join(OUT, "cases.json"), "w") as fh:
         json.dump(dict(generator="tools/gen_golden.py",
                        reference="alfille/pypanadapter @ /root/reference (S, T variants)",
                        numpy=np.__version__, scipy=__import__("scipy").__version__,
-                       cases=cases, waterfall=wf_meta), fh, indent=1)
+                       cases=cases, waterfall=wf_meta, ring=ring_meta), fh, indent=1)
     print("wrote", len(cases), "row cases,", len(wf_meta), "waterfall sequences")
     return 0
 

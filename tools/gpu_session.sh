@@ -1,16 +1,18 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel-trace summary.
-# Every GPU step has its own time limit; a crash/abort/timeout (anything but a plain
-# test failure) ends the session so nothing else touches a possibly faulted GPU.
-# usage: tools/gpu_session.sh <tag> [steps...]   steps: tests smoke bench prof pmc
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel-trace / PMC summaries.
+# Every GPU step has its own time limit; a crash/abort/timeout (anything but a plain test
+# failure) ends the session so nothing else touches a possibly faulted GPU.
+# usage: tools/gpu_session.sh <tag> [steps...]   steps: tests smoke bench quick prof pmc sq cfgs
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 2
-TAG="${1:-r01}"
+TAG="${1:-r02}"
 shift || true
 STEPS="${*:-tests smoke bench prof}"
-OUT="$R/gpurun_out"
+OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
+export TMPDIR=/tmp
+FAST="--no-cpu --no-e2e --no-check"
 
 run() {  # name seconds cmd...
   local name=$1 to=$2
@@ -19,47 +21,48 @@ run() {  # name seconds cmd...
   timeout -k 10 "$to" "$@" >"$OUT/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"
-  tail -n 25 "$OUT/$name.log"
+  tail -n 12 "$OUT/$name.log"
   return $rc
 }
 
 for s in $STEPS; do
   case $s in
     tests)
-      run pytest_gpu 1100 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --timeout 120 --timeout-method thread
+      run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider -rf --timeout 300 --timeout-method thread
+      rc=$?
+      [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
+    tests_k)  # one file/selection: TESTK env
+      run pytest_k 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --timeout 300 --timeout-method thread ${TESTK}
       rc=$?
       [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     smoke)
       run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
-      run bench 600 python bench.py --steps 10 --warmup 2 --cpu-seconds 8 || exit $? ;;
-    ab)
-      run bench_exact 300 python bench.py --steps 5 --warmup 1 --no-cpu --path 1 || exit $?
-      run bench_fused 300 python bench.py --steps 5 --warmup 1 --no-cpu --path 2 || exit $?
-      run bench_xt 300 python bench.py --steps 5 --warmup 1 --no-cpu --path 3 || exit $? ;;
-    sweep)
-      for blk in 512 1024 2048 4096; do
-        run sweep_b$blk 300 python bench.py --steps 5 --warmup 1 --no-cpu --block $blk || exit $?
-      done ;;
-    bench5)
-      run bench_cfg5_f32 600 python bench.py --config cfg5 --steps 5 --warmup 1 --no-cpu || exit $?
-      run bench_cfg5_f16 600 python bench.py --config cfg5 --steps 5 --warmup 1 --no-cpu --in-dtype complex32 || exit $?
-      run bench_cfg2_f16 600 python bench.py --steps 5 --warmup 1 --no-cpu --in-dtype complex32 || exit $?
-      run bench_cfg2_u8 600 python bench.py --steps 5 --warmup 1 --no-cpu --in-dtype cu8 || exit $? ;;
-    bench3)
-      run bench_cfg3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu || exit $? ;;
+      run bench 900 python bench.py || exit $? ;;
+    quick)
+      run quick 300 python bench.py --steps 100 --warmup 3 $FAST || exit $? ;;
+    cfgs)
+      run bench_cfg3 300 python bench.py --config cfg3 --steps 50 --warmup 2 $FAST || exit $?
+      run bench_cfg5 300 python bench.py --config cfg5 --steps 20 --warmup 2 $FAST || exit $?
+      run bench_cfg1 300 python bench.py --config cfg1 --steps 50 --warmup 2 $FAST || exit $?
+      run bench_cfg2_u8 300 python bench.py --in-dtype cu8 --steps 50 --warmup 2 $FAST || exit $? ;;
     prof)
-      export TMPDIR=/tmp
       run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$OUT/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu || exit $? ;;
+        -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 2 $FAST || exit $? ;;
     pmc)
-      export TMPDIR=/tmp
-      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-        -d "$OUT/pmc_fetch_$TAG" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu || exit $?
-      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-        -d "$OUT/pmc_write_$TAG" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu || exit $?
-      python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG" 4096 cfg2 \
-        "$OUT/traffic_cfg2_$TAG.json" xa > /dev/null || exit $? ;;
+      run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+        -d "$OUT/pmc_fetch" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 $FAST || exit $?
+      run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+        -d "$OUT/pmc_write" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 $FAST || exit $?
+      python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" 4096 cfg2 \
+        "$OUT/traffic_cfg2.json" complex64 > "$OUT/traffic.log" || exit $? ;;
+    sq)
+      run pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU \
+        SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT \
+        GRBM_GUI_ACTIVE --output-format csv \
+        -d "$OUT/pmc_sq" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 $FAST || exit $?
+      python3 "$R/tools/sq_counters.py" "$OUT/pmc_sq" 4096 cfg2 complex64 "$OUT/sq_cfg2.json" \
+        > "$OUT/sq.log" || exit $? ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac

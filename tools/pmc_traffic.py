@@ -10,7 +10,10 @@ widths are uncalibrated; both raw and corrected sums are kept.
 Per step = (sum over every zfft dispatch) / (number of Welch row dispatches): each
 process call launches exactly one of welch_rows / welch_dif / welch4_rows.
 
-usage: tools/pmc_traffic.py <fetch_dir> <write_dir> <frames> <config> [out.json] [schedule]
+The summary is stamped with the kernel-source hash (bench.py uses it only while the sources
+are unchanged).
+
+usage: tools/pmc_traffic.py <fetch_dir> <write_dir> <frames> <config> [out.json] [in_dtype]
 """
 import csv
 import glob
@@ -19,6 +22,9 @@ import os
 import re
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pypanadapter_amd import build  # noqa: E402
 
 
 def kname(name: str) -> str:
@@ -29,7 +35,7 @@ def kname(name: str) -> str:
 def load(d, counter):
     per = defaultdict(float)
     count = defaultdict(int)
-    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter and "zfft::" in r["Kernel_Name"]:
                 k = kname(r["Kernel_Name"])
@@ -41,7 +47,7 @@ def load(d, counter):
 def main():
     fetch_dir, write_dir, frames, config = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
     out = sys.argv[5] if len(sys.argv) > 5 else None
-    schedule = sys.argv[6] if len(sys.argv) > 6 else "xa"
+    in_dtype = sys.argv[6] if len(sys.argv) > 6 else "complex64"
     fetch, fc = load(fetch_dir, "FETCH_SIZE")
     write, wc = load(write_dir, "WRITE_SIZE")
     step_kernel = ("welch_rows", "welch_dif", "welch4_rows")
@@ -57,7 +63,8 @@ def main():
                          "hbm_bytes_per_step_fetch_x2": int((2 * f_kib + w_kib) * 1024)}
         tot_raw += (f_kib + w_kib) * 1024
         tot_x2 += (2 * f_kib + w_kib) * 1024
-    res = {"frames": frames, "config": config, "schedule": schedule,
+    res = {"frames": frames, "config": config, "in_dtype": in_dtype,
+           "source_hash": build.source_hash(),
            "steps_counted": [steps_f, steps_w],
            "hbm_bytes_per_step": int(tot_x2), "hbm_bytes_per_step_raw": int(tot_raw),
            "per_kernel": per_kernel,

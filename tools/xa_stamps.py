@@ -23,7 +23,7 @@ def main():
     lib = _lib.load()
     buf = (ctypes.c_ulonglong * 11)()
     with ZoomFFT(4096, 8, 2.4e6) as plan:
-        plan.set_path(4)
+        plan.set_path(3)
         plan.rows(x[:64])
         lib.zfft_debug_xa_stamps(buf)
         plan.rows(x)
