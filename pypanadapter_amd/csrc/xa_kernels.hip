@@ -11,26 +11,32 @@
 //   g = h / D2(1/w)                        backward all-pole cascade, output rate
 //
 // so a stage costs 8 + 12.5 + 4 packed multiply-adds per input sample, against 2 x 17 for
-// two DF2T passes.  A wave walks its frame in tiles of 64 lanes x 32 samples:
-//  forward:   every lane runs the all-pole cascade from a zero state over its 32 samples;
+// two DF2T passes.  A wave walks its frame in tiles of 64 lanes x B samples (B = 32 or 64;
+// lane i owns the sub-block of B consecutive samples, K = B/2 kept outputs):
+//  forward:   every lane runs the all-pole cascade from a zero state over its B samples;
 //             its end state goes to the real modal basis (T^-1, block lower triangular,
 //             one rotation-scaling 2x2 block per pole pair), a Kogge-Stone scan over
-//             lanes -- per mode only as deep as its radius needs (.935 .808 .682 .587 ->
-//             4 2 1 1 levels) -- gives each lane its entering state, and the outputs get
-//             C A^t T m_in.  The tile's entering state is folded into lane 0.
-//  FIR:       the corrected v go to LDS; lane i evaluates h at the 16 odd positions of
-//             [32i - 16, 32i + 16) from v[32i - 24, 32i + 32): its own row and the last
-//             24 samples of row i-1 (row -1 = the previous tile's row 63, kept in LDS).
-//  backward:  the same scheme on the 16 h values of each lane, descending, with the
+//             lanes -- per mode only as deep as its radius needs (xa_levels) -- gives each
+//             lane its entering state, and pass 2 reruns the cascade from it.  The tile's
+//             entering state is folded into lane 0.
+//  FIR:       lane i evaluates h at the K odd positions of [B i - 16, B i + B - 16) from
+//             v[B i - 24, B i + B): its own v and the last 24 v of lane i-1, whose share
+//             lane i-1 accumulates itself and hands over with one DPP shift (lane 0 takes
+//             the previous tile's lane-63 share from LDS).
+//  backward:  the same scheme on the K h values of each lane, descending, with the
 //             state entering the tile from above provisionally zero; the state it leaves
 //             at the tile bottom is exact regardless (its dependence on the top state is
-//             |lambda^2|^512 < 1e-29) and is the top state of the tile below, processed
+//             |lambda^2|^(32 B) < 1e-29) and is the top state of the tile below, processed
 //             one step earlier: that tile's top kXaLag outputs get C A2^d T q, then all
 //             its outputs are stored.
 //  frame end: the forward pre-history is the steady state of constant ext[0]
 //             (sosfilt_zi * ext[0]); the backward post-history is the steady state of
 //             constant f[e-1], f = N v formed explicitly for the last 16 positions, whose
 //             h use the unmerged form N(1/z) D(-1/z) on f clamped at e-1.
+// B = 32 keeps a tile in 256 VGPRs (2 waves/SIMD).  B = 64 would halve the per-tile scan
+// and basis-change work per sample, but its fully unrolled tile is 112 KB of code against
+// the 64 KB instruction cache two CUs share (B = 32: 32 KB): measured 6.6x slower on
+// MI355X, so only B = 32 is instantiated.
 // Numerics: float32, max relative error ~8e-6 of the decimated IQ vs float64 sosfiltfilt
 // (plain float32 sosfiltfilt: ~1e-6); end-to-end rows within 1e-5 dB (tools/xa_proto.py).
 #include <cstddef>
@@ -44,40 +50,23 @@
 namespace zfft {
 namespace xa {
 
-constexpr int kRow = kXaB + 2;          // LDS row stride (v2f): ds_read_b128 rows conflict-free
 constexpr int kHalfRows = 32;           // transposes go through LDS one half tile at a time
-constexpr int kHeldRow = kXaK + 2;      // output-transpose rows (v2f): b128 writes conflict-free
-// + FIR carry (12 used) + frame-end v carry + LO chunk starts
-constexpr int kBuf = kHalfRows * kRow + 16 + 64 + 32;
 constexpr int kWaves = 2;               // waves (frames) per workgroup
-#ifndef XA_WAVES
-#define XA_WAVES 2                      // waves per SIMD the register budget is cut for
-#endif
-#ifndef XA_PF
-#define XA_PF 32                        // input chunks of the next tile loaded a tile ahead
-#endif
-#ifndef XA_SPREAD
-#define XA_SPREAD 1                     // next-tile loads in 8 groups spread over the tile
-#endif
-// diagnostic builds only (results invalid): no stage-output stores / one shared input frame
-#ifndef XA_DIAG_NOSTORE
-#define XA_DIAG_NOSTORE 0
-#endif
-#ifndef XA_DIAG_ONEFRAME
-#define XA_DIAG_ONEFRAME 0
-#endif
-#ifndef XA_LAG_LDS
-#define XA_LAG_LDS 1                    // lag rows copied to LDS once per workgroup
-#endif
-#ifndef XA_LAG_EARLY
-#define XA_LAG_EARLY 1                  // lag rows loaded before the backward pass
-#endif
-#ifndef XA_BUFLOAD
-#define XA_BUFLOAD 1                    // next-tile loads through a range-checked buffer resource
-#endif
-#ifndef XA_ROWSCAN
-#define XA_ROWSCAN 1                    // modal scans on DPP rows + one cross-row step
-#endif
+constexpr int kLagChunks = kXaLag / 64; // held output chunks of a tile
+
+template <int B>
+struct Geo {
+  static constexpr int K = B / 2;            // kept outputs per lane and tile
+  static constexpr int T = 64 * B;           // tile (input samples)
+  static constexpr int kRow = B + 2;         // LDS row stride (v2f): ds_read_b128 rows conflict-free
+  static constexpr int kHeldRow = K + 2;     // output-transpose rows (v2f): b128 writes conflict-free
+  static constexpr int kOutChunks = K;       // 64-output chunks per tile
+  static constexpr int kRowsPerChunk = 64 / B > 0 ? 64 / B : 1;  // input rows one 64-sample chunk fills
+  // LDS per wave: half-tile transposes + FIR carry (12 used) + frame-end v carry (the 64 v
+  // before the last tile) + LO chunk starts (B)
+  static constexpr int kBuf = kHalfRows * kRow + 16 + 64 + B;
+  static constexpr int kWavesPerSimd = B == 32 ? 2 : 1;  // the register budget is cut for
+};
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 // LDS pointers keep their address space (a generic pointer turns every LDS access into a
@@ -85,20 +74,14 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef v2f __attribute__((address_space(3))) *LP;
 typedef v4f __attribute__((address_space(3))) *LP4;
 // Filter tables: scalar (K$) reads of the constant table; the far-field `lag` rows are
-// per-lane vector reads.
+// per-lane reads from an LDS copy.
 typedef const XaTab __attribute__((address_space(4))) *CT;
 // an opaque copy per phase: reads are not hoisted out of the tile loop (which would pin
 // the whole table in SGPRs and spill), each phase re-reads the few it needs
-typedef const XaTab __attribute__((address_space(4))) *CS;  // scalar reads (global copy)
-__device__ __forceinline__ CS fresh_s(CS p) {
-  asm volatile("" : "+s"(p));
-  return p;
-}
 __device__ __forceinline__ CT fresh(CT p) {
   asm volatile("" : "+s"(p));
   return p;
 }
-
 
 // Raw input element of each in_dtype: tile loads are issued one tile ahead and converted
 // only when consumed, so no conversion (and no wait) sits behind the load.
@@ -206,13 +189,12 @@ __device__ __forceinline__ void to_modal(CT tab, const v2f s[8], Md &m) {
   }
 }
 
-// inclusive weighted scan over lanes: UP (lane i sums lanes j <= i) or down (j >= i),
+// Inclusive weighted scan over lanes: UP (lane i sums lanes j <= i) or down (j >= i),
 // m_i = sum_j lambda^(S |i-j|) m_j per mode, every term within the mode's reach exact.
-// XA_ROWSCAN: modes 0, 1 run Kogge-Stone inside 16-lane rows on DPP row shifts, then add
-// the adjacent row's end lane (its within-row inclusive sum) weighted by the lane's own
-// distance to it (xw: c0 s0 c1 s1 for this lane-in-row): UP by DPP row_bcast:15, down by
-// one ds_bpermute round; modes 2, 3 need one whole-wave DPP shift.  Otherwise the older
-// whole-wave form (DPP first level, ds_bpermute chains after).
+// Modes 0, 1 run Kogge-Stone inside 16-lane rows on DPP row shifts, then add the adjacent
+// row's end lane (its within-row inclusive sum) weighted by the lane's own distance to it
+// (xw: c0 s0 c1 s1 for this lane-in-row): UP by DPP row_bcast:15, down by one ds_bpermute
+// round; modes 2, 3 need one whole-wave DPP shift.
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ v2f dpp0(v2f src) {  // lanes without a source (or row) get 0
   if constexpr (ROWMASK == 0xF)  // bound_ctrl: a lane without a source reads 0, no old value
@@ -232,59 +214,65 @@ __device__ __forceinline__ v2f row_shift(v2f src, int d) {  // by 2^d lanes insi
     default: return dpp0<(UP ? kRowShr : kRowShl) + 8, 0xF>(src);
   }
 }
-template <int PASS, bool UP>
+template <int B, int PASS, bool UP>
 __device__ __forceinline__ void modal_scan(Md &m, CT tab, int lane, v4f xw) {
   asm volatile("" : "+v"(lane));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
-    for (int d = 0; d < kXaLevels[j]; ++d) {
+    for (int d = 0; d < xa_levels(B, j); ++d) {
       CT t = fresh(tab);
-      float c = pass_of<PASS>(t).scan[d][j][0], sn = pass_of<PASS>(t).scan[d][j][1];
+      const float c = pass_of<PASS>(t).scan[d][j][0], sn = pass_of<PASS>(t).scan[d][j][1];
       v2f pa, pb;
-      if (XA_ROWSCAN && j < kXaRowModes) {
+      if (j < kXaRowModes) {
         pa = row_shift<UP>(m.r[2 * j], d);
         pb = row_shift<UP>(m.r[2 * j + 1], d);
-      } else if (d == 0) {
+      } else {  // one level: a whole-wave shift by one lane
         constexpr int ctrl = UP ? kShr1 : kShl1;
         pa = dpp0<ctrl, 0xF>(m.r[2 * j]);
         pb = dpp0<ctrl, 0xF>(m.r[2 * j + 1]);
-      } else {
-        const int sh = 1 << d;
-        const bool take = UP ? lane >= sh : lane + sh <= 63;
-        const int src = (UP ? lane - sh : lane + sh) & 63;
-        pa = shfl2(m.r[2 * j], src);
-        pb = shfl2(m.r[2 * j + 1], src);
-        c = take ? c : 0.f;
-        sn = take ? sn : 0.f;
       }
       rot(pa, pb, c, sn);
       m.r[2 * j] += pa;
       m.r[2 * j + 1] += pb;
     }
   }
-  if (XA_ROWSCAN) {
-    v2f pa[kXaRowModes], pb[kXaRowModes];
+  v2f pa[kXaRowModes], pb[kXaRowModes];
 #pragma unroll
-    for (int j = 0; j < kXaRowModes; ++j) {
-      if (UP) {  // rows 1..3 <- lane 15 of the row below
-        pa[j] = dpp0<kRowBcast15, 0xE>(m.r[2 * j]);
-        pb[j] = dpp0<kRowBcast15, 0xE>(m.r[2 * j + 1]);
-      } else {   // rows 0..2 <- lane 0 of the row above
-        const int src = ((lane | 15) + 1) & 63;
-        pa[j] = shfl2(m.r[2 * j], src);
-        pb[j] = shfl2(m.r[2 * j + 1], src);
-      }
-    }
-    const bool take = UP || lane < 48;
-#pragma unroll
-    for (int j = 0; j < kXaRowModes; ++j) {
-      const float c = take ? (j == 0 ? xw.x : xw.z) : 0.f, sn = take ? (j == 0 ? xw.y : xw.w) : 0.f;
-      rot(pa[j], pb[j], c, sn);
-      m.r[2 * j] += pa[j];
-      m.r[2 * j + 1] += pb[j];
+  for (int j = 0; j < kXaRowModes; ++j) {
+    if (UP) {  // rows 1..3 <- lane 15 of the row below
+      pa[j] = dpp0<kRowBcast15, 0xE>(m.r[2 * j]);
+      pb[j] = dpp0<kRowBcast15, 0xE>(m.r[2 * j + 1]);
+    } else {   // rows 0..2 <- lane 0 of the row above
+      const int src = ((lane | 15) + 1) & 63;
+      pa[j] = shfl2(m.r[2 * j], src);
+      pb[j] = shfl2(m.r[2 * j + 1], src);
     }
   }
+  const bool take = UP || lane < 48;
+#pragma unroll
+  for (int j = 0; j < kXaRowModes; ++j) {
+    const float c = take ? (j == 0 ? xw.x : xw.z) : 0.f, sn = take ? (j == 0 ? xw.y : xw.w) : 0.f;
+    rot(pa[j], pb[j], c, sn);
+    m.r[2 * j] += pa[j];
+    m.r[2 * j + 1] += pb[j];
+  }
+}
+
+// The table pointer, but only once v is computed: scalar reads through it cannot be
+// hoisted above v (the scheduler would otherwise issue every row's reads at once and spill).
+__device__ __forceinline__ CT after(CT p, v2f v) {
+  asm volatile("" : "+s"(p) : "v"(v));
+  return p;
+}
+
+// acc + sum_r row[r] m_r: one output's zero-input response to a modal state (row: 8 floats,
+// read by scalar loads)
+__device__ __forceinline__ v2f add_modal(v2f acc, const float __attribute__((address_space(4))) *row,
+                                         const Md &m) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) acc = vfma(splat(row[r]), m.r[r], acc);
+  return acc;
 }
 
 // the state entering a lane, rotated over one sub-block and folded into that lane's end
@@ -319,30 +307,15 @@ __device__ unsigned long long g_xa_stamps[kStampSegs + 1];
 #define XA_STAMP(i)
 #endif
 
-// modal -> DF-I state, s = T m (T block lower triangular: section k from modes <= k)
-template <int PASS>
-__device__ __forceinline__ void from_modal(CT tab, const Md &m, v2f s[8]) {
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    CT t = fresh(tab);
-    v2f acc = splat(0.f);
-#pragma unroll
-    for (int q = 0; q < (r | 1) + 1; ++q) acc = vfma(splat(pass_of<PASS>(t).t[r][q]), m.r[q], acc);
-    s[r] = acc;
-  }
-}
-
-template <bool MIX, int DT, int FLIP>
-__global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc in, int n,
-                                                                        const v2f *__restrict__ lo,
-                                                                        v2f *__restrict__ out, int frames,
-                                                                        const XaTab *tab_g) {
-  __shared__ __attribute__((aligned(16))) v2f lds_all[kWaves][kBuf];
+template <int B, bool MIX, int DT, int FLIP>
+__global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_kernel(
+    InDesc in, int n, const v2f *__restrict__ lo, v2f *__restrict__ out, int frames, const XaTab *tab_g) {
+  using G = Geo<B>;
+  constexpr int K = G::K, T = G::T, kRow = G::kRow, kHeldRow = G::kHeldRow, kChunks = G::kOutChunks;
+  __shared__ __attribute__((aligned(16))) v2f lds_all[kWaves][G::kBuf];
   const CT tab = (CT)tab_g;
-#if XA_LAG_LDS
-  __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];
+  __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];  // lag rows, copied once
   for (int i = threadIdx.x; i < kXaLag * 2; i += 64 * kWaves) lag_l[i] = ((const v4f *)tab_g->lag)[i];
-#endif
   __shared__ v4f xw_l[2][16];  // cross-row scan weights (XaPass::xr), forward / backward
   if (threadIdx.x < 32) xw_l[threadIdx.x >> 4][threadIdx.x & 15] = ((const v4f *)((threadIdx.x >> 4) ? tab_g->b.xr : tab_g->f.xr))[threadIdx.x & 15];
   __syncthreads();
@@ -353,10 +326,10 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
   const LP buf0 = (LP)lds_all[wv];           // half-tile transposes: 32 rows of kRow v2f
   LP buf = buf0;
   LP pcarry = buf + kHalfRows * kRow;       // lane 63's FIR neighbour part, for next lane 0
-  LP vcarry = pcarry + 16;                  // rows 62, 63 of the tile before the last
-  LP cq = vcarry + 64;                      // lo at the 32 chunk starts of the tile
+  LP vcarry = pcarry + 16;                  // the 64 v before the last tile
+  LP cq = vcarry + 64;                      // lo at the B chunk starts of the tile
   const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
-  const int nt = (e + 15) / kXaT + 1;  // the last FIR/backward tile reaches e - 1
+  const int nt = (e + 15) / T + 1;  // the last FIR/backward tile reaches e - 1
   v2f *__restrict__ o = out + (int64_t)f * n_out;
   auto X = [&](int i) -> v2f {
     v2f v = load_in_t<DT, FLIP>(in, f, i);
@@ -376,7 +349,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
   for (int r = 0; r < 8; ++r) m_in.r[r] = tab->f.ss[r] * x0;
   {  // v pre-history (steady output for constant ext[0]): the FIR part lane -1 owes lane 0
     const v2f vs = tab->vss * x0;
-    if (lane < kXaK) {
+    if (lane < 12) {
       CT tb = fresh(tab);
       v2f acc = splat(0.f);
       for (int t = 0; t < 25; ++t)  // taps on W[m], 1 <= m <= 23, of output k = lane
@@ -387,9 +360,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
   }
   __builtin_amdgcn_wave_barrier();
 
-  constexpr int kChunks = kXaT / 2 / 64;
-  constexpr int kLagChunks = kXaLag / 64;
-  auto m_of = [&](int tile, int idx) { return tile * (kXaT / 2) - (kPad + 15) / 2 + idx; };
+  auto m_of = [&](int tile, int idx) { return tile * (T / 2) - (kPad + 15) / 2 + idx; };
   // Tile outputs -> frame row through LDS transposes (64 consecutive outputs per store
   // instruction), one half tile at a time.  Chunks below the top kXaLag outputs are final
   // at once; the top chunks wait in registers for the next tile's exact top state q.
@@ -399,34 +370,33 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
   auto flush_tile = [&](int tile, const v2f *h, int ln) {
     const int m0 = m_of(tile, ln);
     v2f *__restrict__ od = o + m0;
-    const bool inside = m_of(tile, 0) >= 0 && m_of(tile, kXaT / 2) <= n_out;  // wave-uniform
+    const bool inside = m_of(tile, 0) >= 0 && m_of(tile, T / 2) <= n_out;  // wave-uniform
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      if ((ln >> 5) == hf) {  // lanes of this half: 16 outputs each into row ln % 32
+      if ((ln >> 5) == hf) {  // lanes of this half: K outputs each into row ln % 32
         LP4 hw = (LP4)(buf + (ln & 31) * kHeldRow);
 #pragma unroll
-        for (int k = 0; k < kXaK / 2; ++k) hw[k] = v4f{h[2 * k].x, h[2 * k].y, h[2 * k + 1].x, h[2 * k + 1].y};
+        for (int k = 0; k < K / 2; ++k) hw[k] = v4f{h[2 * k].x, h[2 * k].y, h[2 * k + 1].x, h[2 * k + 1].y};
       }
       __builtin_amdgcn_wave_barrier();
-      // output idx = 64 c + ln (c in this half) sits at row idx/16 - 32 hf, column ln % 16;
+      // output idx = 64 c + ln (c in this half) sits at row idx/K - 32 hf, column idx % K;
       // all the half's chunks are read first (one LDS round trip), then stored: an interior
       // tile (wave-uniform `inside`) stores without per-chunk tests
-      const LP hr = buf + (ln >> 4) * kHeldRow + (ln & 15);
+      const LP hr = buf + (ln / K) * kHeldRow + (ln % K);
       v2f vc[kChunks / 2];
 #pragma unroll
-      for (int cc = 0; cc < kChunks / 2; ++cc) vc[cc] = hr[cc * 4 * kHeldRow];
+      for (int cc = 0; cc < kChunks / 2; ++cc) vc[cc] = hr[cc * (64 / K) * kHeldRow];
       if (inside) {
 #pragma unroll
         for (int cc = 0; cc < kChunks / 2; ++cc) {
           const int c = hf * (kChunks / 2) + cc;
-          if (c < kChunks - kLagChunks && !XA_DIAG_NOSTORE) od[64 * c] = vc[cc];
+          if (c < kChunks - kLagChunks) od[64 * c] = vc[cc];
         }
       } else {
 #pragma unroll
         for (int cc = 0; cc < kChunks / 2; ++cc) {
           const int c = hf * (kChunks / 2) + cc;
-          if (c < kChunks - kLagChunks && m0 + 64 * c >= 0 && m0 + 64 * c < n_out && !XA_DIAG_NOSTORE)
-            od[64 * c] = vc[cc];
+          if (c < kChunks - kLagChunks && m0 + 64 * c >= 0 && m0 + 64 * c < n_out) od[64 * c] = vc[cc];
         }
       }
 #pragma unroll
@@ -459,60 +429,40 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     const bool inside = m_of(tile, (kChunks - kLagChunks) * 64) >= 0 && m_of(tile, kChunks * 64) <= n_out;
     if (inside) {
 #pragma unroll
-      for (int c = 0; c < kLagChunks; ++c)
-        if (!XA_DIAG_NOSTORE) o[m0 + 64 * c] = held[c];
+      for (int c = 0; c < kLagChunks; ++c) o[m0 + 64 * c] = held[c];
     } else {
 #pragma unroll
       for (int c = 0; c < kLagChunks; ++c) {
         const int m = m0 + 64 * c;
-        if (m >= 0 && m < n_out && !XA_DIAG_NOSTORE) o[m] = held[c];
+        if (m >= 0 && m < n_out) o[m] = held[c];
       }
     }
   };
 
-  // coalesced tile loads: sample s = 64 q + lane of the tile -> row s/32, in two halves; a
-  // fast tile (inside [27, n + 27): no odd extension) is loaded during the previous tile
+  // coalesced tile loads: sample s = 64 q + lane of the tile -> row s/B, col s%B, in two
+  // halves of 32 rows; a fast tile (inside [27, n + 27): no odd extension) is loaded during
+  // the previous tile, through a range-checked buffer resource over the frame, for every
+  // tile (out-of-range lanes read 0; an edge tile never reads them): the prefetch registers
+  // are then dead between their use at the tile start and their reload
   typedef typename Raw<DT>::T RawT;
-  // (XA_DIAG_ONEFRAME: every wave reads frame 0, an L2/MALL-resident input -- diagnostic)
-  const RawT *__restrict__ src = (const RawT *)in.p + (XA_DIAG_ONEFRAME ? 0 : (int64_t)f * in.stride);
-  auto fast_tile = [&](int b) { return b >= kPad && b + kXaT <= n + kPad; };
+  const RawT *__restrict__ src = (const RawT *)in.p + (int64_t)f * in.stride;
+  auto fast_tile = [&](int b) { return b >= kPad && b + T <= n + kPad; };
   v2f wl = splat(0.f);  // lo[n0 + l] = lo[n0] w^l: w^l = lo[l] / sqrt(2), per lane
   if constexpr (MIX) wl = lo[lane] * 0.70710678118654752f;
-  v2f cqv = splat(0.f);  // lo[next tile start - 27 + 64 (lane % 32)], loaded a tile ahead
-  // chunks [0, XA_PF) are loaded a tile ahead (loop-carried registers); the rest are loaded
-  // at the tile start into registers local to the iteration (so they are not carried, and
-  // not held, across the whole loop)
-  constexpr int kPfc = XA_PF > 0 ? XA_PF : 1;
-  RawT pf[kPfc];
-  // next-tile loads: group g = chunks [4g, 4g + 4), issued at 8 points of the tile
-  const RawT *pnext = src;
+  v2f cqv = splat(0.f);  // lo[next tile start - 27 + 64 (lane % B)], loaded a tile ahead
+  RawT pf[B];            // the next tile's B input chunks
   bool next_fast = false;
   int next_i0 = 0;  // first input index of the next tile
-#if XA_BUFLOAD
-  // next-tile loads through a range-checked buffer resource over the frame, issued for
-  // every tile (out-of-range lanes read 0; an edge tile never reads them): pf is then dead
-  // between its use at the tile start and its reload, where a conditional reload would
-  // keep all of pf live across the whole tile
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void *)src, (short)0, (int)(in.len * (int64_t)sizeof(RawT)), 0x00020000);
   uint32_t next_off = 0;  // byte offset of this lane's element of the next tile's chunk 0
+  // next-tile loads: group g = chunks [g B/8, (g+1) B/8), issued at 8 points of the tile
   auto issue_group = [&](int g) {
-    if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + 64 * (lane & 31)];
-    if (XA_SPREAD && 4 * g < XA_PF) {
+    if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + 64 * (lane % B)];
 #pragma unroll
-      for (int q = 4 * g; q < 4 * g + 4 && q < XA_PF; ++q)
-        pf[q < kPfc ? q : 0] = buf_load<RawT>(rsrc, next_off + (uint32_t)((FLIP ? -64 : 64) * q * (int)sizeof(RawT)));
-    }
+    for (int q = g * (B / 8); q < (g + 1) * (B / 8); ++q)
+      pf[q] = buf_load<RawT>(rsrc, next_off + (uint32_t)((FLIP ? -64 : 64) * q * (int)sizeof(RawT)));
   };
-#else
-  auto issue_group = [&](int g) {
-    if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + 64 * (lane & 31)];
-    if (XA_SPREAD && next_fast && 4 * g < XA_PF) {
-#pragma unroll
-      for (int q = 4 * g; q < 4 * g + 4 && q < XA_PF; ++q) pf[q < kPfc ? q : 0] = pnext[FLIP ? -64 * q : 64 * q];
-    }
-  };
-#endif
 
 #if XA_STAMPS
   unsigned long long st_acc[kStampSegs] = {}, t_prev;
@@ -531,22 +481,18 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
       vcarry = pcarry + 16;
       cq = vcarry + 64;
     }
-    const int base = tau * kXaT;
+    const int base = tau * T;
     const bool last = tau == nt - 1;
-    v2f y[kXaB];
+    v2f y[B];
     {
       const bool fast = fast_tile(base);  // wave-uniform
-      // chunks not loaded a tile ahead: the first half now, the second half as soon as
-      // the first is in LDS (32 raw VGPRs in flight at a time)
-      const int i0 = base - kPad + ln;
-      const RawT *pcur = src + (FLIP ? in.len - 1 - i0 : i0);
-      LP st = buf + (ln >> 5) * kRow + (ln & 31);
+      LP st = buf + (ln / B) * kRow + (ln % B);
       auto read_rows = [&](int hf) {  // lanes of half hf take their rows
         __builtin_amdgcn_wave_barrier();
         if ((ln >> 5) == hf) {
           const LP4 rp = (LP4)(buf + (ln & 31) * kRow);
 #pragma unroll
-          for (int t = 0; t < kXaB / 2; ++t) {
+          for (int t = 0; t < B / 2; ++t) {
             const v4f w = rp[t];
             y[2 * t] = v2f{w.x, w.y};
             y[2 * t + 1] = v2f{w.z, w.w};
@@ -557,28 +503,18 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
       // the fast and the edge path are separate blocks end to end: raw registers of the
       // fast path never live across the edge path's code (which would force their spill)
       if (fast) {
-        RawT pl[kXaB - XA_PF > 0 ? kXaB - XA_PF : 1];
-        if (XA_PF < kXaB / 2) {
-#pragma unroll
-          for (int q = XA_PF; q < kXaB / 2; ++q) pl[q - XA_PF] = pcur[FLIP ? -64 * q : 64 * q];
-        }
         if (MIX) {
-          if (ln < 32) cq[ln] = cqv;
+          if (ln < B) cq[ln] = cqv;
           __builtin_amdgcn_wave_barrier();
         }
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-          for (int qq = 0; qq < kXaB / 2; ++qq) {
-            const int q = hf * (kXaB / 2) + qq;
-            v2f x = cvt_raw<DT>(q < XA_PF ? pf[q < kPfc ? q : 0] : pl[q >= XA_PF ? q - XA_PF : 0]);
+          for (int qq = 0; qq < B / 2; ++qq) {
+            const int q = hf * (B / 2) + qq;
+            v2f x = cvt_raw<DT>(pf[q]);
             if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl));
-            st[2 * kRow * qq] = x;
-          }
-          if (hf == 0 && XA_PF < kXaB) {
-            __builtin_amdgcn_sched_barrier(0);  // keep these loads behind the first half's use
-#pragma unroll
-            for (int q = (XA_PF > kXaB / 2 ? XA_PF : kXaB / 2); q < kXaB; ++q) pl[q - XA_PF] = pcur[FLIP ? -64 * q : 64 * q];
+            st[G::kRowsPerChunk * kRow * qq] = x;
           }
           read_rows(hf);
         }
@@ -586,102 +522,114 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll 4
-          for (int qq = 0; qq < kXaB / 2; ++qq) st[2 * kRow * qq] = ext(base + ln + 64 * (hf * (kXaB / 2) + qq));
+          for (int qq = 0; qq < B / 2; ++qq) st[G::kRowsPerChunk * kRow * qq] = ext(base + ln + 64 * (hf * (B / 2) + qq));
           read_rows(hf);
         }
       }
     }
-    next_fast = tau + 1 < nt && fast_tile(base + kXaT);  // wave-uniform
-    next_i0 = base + kXaT - kPad;
+    next_fast = tau + 1 < nt && fast_tile(base + T);  // wave-uniform
+    next_i0 = base + T - kPad;
     {
-      const int i0 = base + kXaT - kPad + ln;
-      pnext = src + (FLIP ? in.len - 1 - i0 : i0);
-#if XA_BUFLOAD
+      const int i0 = base + T - kPad + ln;
       next_off = (uint32_t)((FLIP ? in.len - 1 - i0 : (int64_t)i0) * (int64_t)sizeof(RawT));
-#endif
     }
+    // the next tile's loads: groups 0-3 now, 4-5 after the forward pass, 6-7 after the scan
+    // (later issue points leave the register allocator room it does not use: spills)
     issue_group(0);
+    issue_group(1);
+    issue_group(2);
+    issue_group(3);
     XA_STAMP(0);
 
-    // ---- forward all-pole cascade: pass 1 (zero state, end state only), modal scan over
-    //      lanes, pass 2 from the exact entering state, streaming the FIR ----
-    v2f h[kXaK];
+    // ---- forward all-pole cascade: one pass from a zero state streaming the FIR (v0 -> h
+    //      and the neighbour share P); the modal scan over lanes then gives each lane its
+    //      exact entering state, whose zero-input response C A^t T m enters h and P through
+    //      the tables gown / gnb (the FIR of it, precomputed) instead of a second pass ----
+    v2f h[K];
+    Md me;  // state entering this ln's sub-block
     {
-      Md me;  // state entering this ln's sub-block
+      v2f P[12];
+#pragma unroll
+      for (int k = 0; k < K; ++k) h[k] = splat(0.f);
+#pragma unroll
+      for (int k = 0; k < 12; ++k) P[k] = splat(0.f);
       {
         Md m;
         {
           float a1[4], a2[4];
-          load_ap<0>(tab, a1, a2);
           v2f s[8];
 #pragma unroll
           for (int r = 0; r < 8; ++r) s[r] = splat(0.f);
+          // the pass + FIR constants as SGPRs (wide scalar loads): this phase holds the
+          // most VGPRs of the tile
+          const CT tbs = fresh(tab);
 #pragma unroll
-          for (int t = 0; t < kXaB; ++t) (void)ap_step(y[t], s, a1, a2);
+          for (int k = 0; k < 4; ++k) {
+            a1[k] = tbs->f.a1[k];
+            a2[k] = tbs->f.a2[k];
+          }
+          float m25s[25];
+#pragma unroll
+          for (int t = 0; t < 25; ++t) m25s[t] = tbs->m25[t];
+#pragma unroll
+          for (int t = 0; t < B; ++t) {
+            const v2f v = ap_step(y[t], s, a1, a2);
+            y[t] = v;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              const int tap = 24 + t - 1 - 2 * k;
+              if (tap >= 0 && tap < 25) h[k] = vfma(splat(m25s[tap]), v, h[k]);
+            }
+          }
           to_modal<0>(tab, s, m);
+          // this lane's share of its right neighbour's outputs: W[m] = v[B - 24 + m],
+          // 1 <= m < 24
+#pragma unroll
+          for (int t = B - 23; t < B; ++t) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+              const int tap = t - (B - 24) - 1 - 2 * k;
+              if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), y[t], P[k]);
+            }
+          }
+          // frame end: the 64 v before the last tile (lanes 64 - 64/B .. 63 of the tile
+          // before it) and the last tile's two lanes around e-25 .. e-1 go to LDS for
+          // f = N v -- v0 now (y dies here), the entering state's part once it is known
+          // (`ln`: an opaque ln id, so these once-per-frame addresses are not hoisted)
+          if (tau >= nt - 2) {
+            const int la = max(0, (e - 25 - base) / B);
+            if ((!last && ln >= 64 - 64 / B) || (last && (ln == la || ln == la + 1))) {
+              // (no null test on an LDS pointer: LDS address 0 is this workgroup's first row)
+              LP4 wp = (LP4)(last ? buf + (ln - la) * kRow : vcarry + (ln - (64 - 64 / B)) * B);
+#pragma unroll
+              for (int t = 0; t < B / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
+            }
+          }
         }
         XA_STAMP(1);
-        issue_group(1);
+        issue_group(4);
+        issue_group(5);
         fold_entering<0>(m, m_in, tab, ln == 0);
-        modal_scan<0, true>(m, tab, ln, xw_l[0][ln & 15]);
+        modal_scan<B, 0, true>(m, tab, ln, xw_l[0][ln & 15]);
 #pragma unroll
         for (int r = 0; r < 8; ++r) me.r[r] = wave_shift<kShr1>(m_in.r[r], m.r[r]);
 #pragma unroll
         for (int r = 0; r < 8; ++r) m_in.r[r] = lane_of(m.r[r], 63);  // next tile's entering state
       }
       XA_STAMP(2);
-      issue_group(2);
-      // FIR at the 16 odd positions p_k = base + 32 ln - 15 + 2k:
-      //   h_k = sum_t M_t W[2k + t + 1],  W[m] = v(32 ln - 24 + m);
-      // W[24 + t] = this ln's v[t]; W[m < 24] = ln-1's v[8 + m], whose share of h_k
-      // ln-1 accumulates itself (P) and hands over with one DPP shift
-      v2f P[12];
+      issue_group(6);
+      issue_group(7);
+      // + the entering state's response through the FIR (own outputs, neighbour share);
+      // row k's constants are read once output k-4 is done (at most 4 rows in flight)
 #pragma unroll
-      for (int k = 0; k < kXaK; ++k) h[k] = splat(0.f);
+      for (int k = 0; k < K; ++k) {
+        const CT t = k >= 4 ? after(tab, h[k - 4]) : fresh(tab);
+        h[k] = add_modal(h[k], t->gown[k], me);
+      }
 #pragma unroll
-      for (int k = 0; k < 12; ++k) P[k] = splat(0.f);
-      {
-        float a1[4], a2[4];
-        v2f s[8];
-        from_modal<0>(tab, me, s);
-        // the pass-2 + FIR constants as SGPRs (4 wide scalar loads): this phase holds the
-        // most VGPRs of the tile
-        const CS tbs = fresh_s((CS)tab_g);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          a1[k] = tbs->f.a1[k];
-          a2[k] = tbs->f.a2[k];
-        }
-        float m25s[25];
-#pragma unroll
-        for (int t = 0; t < 25; ++t) m25s[t] = tbs->m25[t];
-#pragma unroll
-        for (int t = 0; t < kXaB; ++t) {
-          // the rest of the next tile's loads go out during pass 2, ahead of the lag rows
-          // (finish_held waits on those; vmcnt counts in issue order)
-          if (t == 4) issue_group(3);
-          if (t == 10) issue_group(4);
-          if (t == 16) issue_group(5);
-          if (t == 22) issue_group(6);
-          if (t == 28) issue_group(7);
-          const v2f v = ap_step(y[t], s, a1, a2);
-          y[t] = v;
-#pragma unroll
-          for (int k = 0; k < kXaK; ++k) {
-            const int tap = 24 + t - 1 - 2 * k;
-            if (tap >= 0 && tap < 25) h[k] = vfma(splat(m25s[tap]), v, h[k]);
-          }
-        }
-        // this lane's share of its right neighbour's outputs: W[m] = v[8 + m], 1 <= m < 24
-        // (after pass 2, so the pass's state registers are free)
-#pragma unroll
-        for (int t = 9; t < kXaB; ++t) {
-#pragma unroll
-          for (int k = 0; k < 12; ++k) {
-            const int tap = t - 8 - 1 - 2 * k;
-            if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), y[t], P[k]);
-          }
-        }
+      for (int k = 0; k < 12; ++k) {
+        const CT t = after(tab, k >= 4 ? P[k - 4] : h[K - 4 + k]);
+        P[k] = add_modal(P[k], t->gnb[k], me);
       }
       {  // neighbour shares: ln i takes ln i-1's P, ln 0 the previous tile's ln 63's
         const LP4 pc = (LP4)pcarry;
@@ -700,44 +648,21 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
       }
     }
     XA_STAMP(3);
-    // frame end: v of the tile before the last (rows 62, 63) and of the last tile's two
-    // lanes around e-25 .. e-1 go to LDS for f = N v.  (`ln`: an opaque ln id, so the
-    // addresses of these once-per-frame paths are not hoisted out of the loop.)
-    const int la = max(0, (e - 25 - base) >> 5);
-    if (tau >= nt - 2) {
-      // (no null test on an LDS pointer: LDS address 0 is this workgroup's first row)
-      LP dst = buf;
-      bool put = false;
-      if (!last && ln >= 62) {
-        dst = vcarry + (ln - 62) * 32;
-        put = true;
-      }
-      if (last && (ln == la || ln == la + 1)) {
-        dst = buf + (ln - la) * kRow;
-        put = true;
-      }
-      if (put) {
-        LP4 wp = (LP4)dst;
+    const int la = max(0, (e - 25 - base) / B);
+    if (tau >= nt - 2 && ((!last && ln >= 64 - 64 / B) || (last && (ln == la || ln == la + 1)))) {
+      // v = v0 + C A^t T me on the rows stored after the pass
+      LP wp = last ? buf + (ln - la) * kRow : vcarry + (ln - (64 - 64 / B)) * B;
+#pragma unroll 4
+      for (int t = 0; t < B; ++t) {
+        CT tb = fresh(tab);
+        v2f acc = wp[t];
 #pragma unroll
-        for (int t = 0; t < kXaB / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
+        for (int r = 0; r < 8; ++r) acc = vfma(splat(tb->fcat[t][r]), me.r[r], acc);
+        wp[t] = acc;
       }
     }
     __builtin_amdgcn_wave_barrier();
-    // lag rows for the held tile's top outputs, then the next tile's loads: both land
-    // while the backward pass runs
     v4f lg[2 * kLagChunks];
-    if (!XA_LAG_LDS && XA_LAG_EARLY && tau > 0) {
-#pragma unroll
-      for (int c = 0; c < kLagChunks; ++c) {
-        const v4f *lr = (const v4f *)&tab_g->lag[kXaLag - 1 - 64 * c - ln][0];
-        lg[2 * c] = lr[0];
-        lg[2 * c + 1] = lr[1];
-      }
-    }
-    if (!XA_SPREAD && next_fast) {
-#pragma unroll
-      for (int q = 0; q < XA_PF; ++q) pf[q < kPfc ? q : 0] = pnext[FLIP ? -64 * q : 64 * q];
-    }
     XA_STAMP(4);
     v2f h_ss = splat(0.f);  // backward steady input (last tile only)
     if (last) {
@@ -745,7 +670,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
       // lane 0..15; h at the odd j in (e-17, e-1] in the unmerged form, one per lane 0..7
       auto v_at = [&](int p) -> v2f {
         const int r = p - base;
-        return r < 0 ? vcarry[64 + r] : buf[((r >> 5) - la) * kRow + (r & 31)];
+        return r < 0 ? vcarry[64 + r] : buf[(r / B - la) * kRow + (r % B)];
       };
       LP fbuf = buf + 2 * kRow, tbuf = buf + 3 * kRow;
       if (ln < 16) {
@@ -770,8 +695,8 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int k = 0; k < kXaK; ++k) {
-        const int j = base + 32 * ln - 15 + 2 * k;
+      for (int k = 0; k < K; ++k) {
+        const int j = base + B * ln - 15 + 2 * k;
         if (j > e - 1) h[k] = h_ss;
         else if (j > e - 17) h[k] = tbuf[(j - j0) >> 1];
       }
@@ -779,8 +704,9 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
     }
     XA_STAMP(5);
 
-    // ---- backward all-pole cascade on h, descending (ln 63 holds the tile top):
-    //      pass 1, scan down, pass 2 from the exact entering state ----
+    // ---- backward all-pole cascade on h, descending (ln 63 holds the tile top): one pass
+    //      from a zero state, the scan down, then the entering state's zero-input response
+    //      C A2^d T q (the first rows of the lag table) added to each output ----
     Md q_exit;
     {
       Md qe;
@@ -793,7 +719,7 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
 #pragma unroll
           for (int r = 0; r < 8; ++r) s[r] = splat(0.f);
 #pragma unroll
-          for (int k = kXaK - 1; k >= 0; --k) (void)ap_step(h[k], s, a1, a2);
+          for (int k = K - 1; k >= 0; --k) h[k] = ap_step(h[k], s, a1, a2);
           to_modal<1>(tab, s, m);
         }
         XA_STAMP(6);
@@ -804,39 +730,27 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
           for (int r = 0; r < 8; ++r) qtop.r[r] = last ? tb->b.ss[r] * h_ss : splat(0.f);
         }
         if (last) fold_entering<1>(m, qtop, tab, ln == 63);
-        modal_scan<1, false>(m, tab, ln, xw_l[1][ln & 15]);
+        modal_scan<B, 1, false>(m, tab, ln, xw_l[1][ln & 15]);
 #pragma unroll
         for (int r = 0; r < 8; ++r) qe.r[r] = wave_shift<kShl1>(qtop.r[r], m.r[r]);
 #pragma unroll
         for (int r = 0; r < 8; ++r) q_exit.r[r] = lane_of(m.r[r], 0);
       }
-      float a1[4], a2[4];
-      load_ap<1>(tab, a1, a2);
-      v2f s[8];
-      from_modal<1>(tab, qe, s);
 #pragma unroll
-      for (int k = kXaK - 1; k >= 0; --k) h[k] = ap_step(h[k], s, a1, a2);
+      for (int k = K - 1; k >= 0; --k) {
+        const CT t = k < K - 4 ? after(tab, h[k + 4]) : fresh(tab);
+        h[k] = add_modal(h[k], t->lag[K - 1 - k], qe);
+      }
     }
     XA_STAMP(7);
     // ---- the tile below is complete: its top state is this tile's bottom state ----
     if (tau > 0) {
-#if XA_LAG_LDS
 #pragma unroll
       for (int c = 0; c < kLagChunks; ++c) {
         const int d = kXaLag - 1 - 64 * c - ln;
         lg[2 * c] = lag_l[2 * d];
         lg[2 * c + 1] = lag_l[2 * d + 1];
       }
-#else
-      if (!XA_LAG_EARLY) {
-#pragma unroll
-        for (int c = 0; c < kLagChunks; ++c) {
-          const v4f *lr = (const v4f *)&tab_g->lag[kXaLag - 1 - 64 * c - ln][0];
-          lg[2 * c] = lr[0];
-          lg[2 * c + 1] = lr[1];
-        }
-      }
-#endif
       finish_held(tau - 1, &q_exit, lg, ln);
     }
     XA_STAMP(8);
@@ -853,18 +767,37 @@ __global__ __launch_bounds__(64 * kWaves, XA_WAVES) void xa_stage_kernel(InDesc 
 #endif
 }
 
-template <bool MIX, int DT, int FLIP>
+template <int B, bool MIX, int DT, int FLIP>
 static void xa_launch(const InDesc &in, int n, const float2 *lo, float2 *out, int frames,
                       const XaTab *tab, hipStream_t st) {
-  hipLaunchKernelGGL((xa_stage_kernel<MIX, DT, FLIP>), dim3((unsigned)((frames + kWaves - 1) / kWaves)),
+  hipLaunchKernelGGL((xa_stage_kernel<B, MIX, DT, FLIP>), dim3((unsigned)((frames + kWaves - 1) / kWaves)),
                      dim3(64 * kWaves), 0, st, in, n, (const v2f *)lo, (v2f *)out, frames, tab);
+}
+
+template <int B>
+static hipError_t xa_dispatch(const InDesc &in, int n, const float2 *lo, bool mix, float2 *out,
+                              int frames, const XaTab *tab, hipStream_t st) {
+  if (!mix) {
+    if (in.dtype != kInC64 || in.flip) return hipErrorInvalidValue;  // stages >= 1: internal
+    xa_launch<B, false, kInC64, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInC64) {
+    if (in.flip) xa_launch<B, true, kInC64, 1>(in, n, lo, out, frames, tab, st);
+    else xa_launch<B, true, kInC64, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInC32H) {
+    if (in.flip) xa_launch<B, true, kInC32H, 1>(in, n, lo, out, frames, tab, st);
+    else xa_launch<B, true, kInC32H, 0>(in, n, lo, out, frames, tab, st);
+  } else if (in.dtype == kInF32R) {
+    if (in.flip) xa_launch<B, true, kInF32R, 1>(in, n, lo, out, frames, tab, st);
+    else xa_launch<B, true, kInF32R, 0>(in, n, lo, out, frames, tab, st);
+  } else {
+    if (in.flip) xa_launch<B, true, kInCU8, 1>(in, n, lo, out, frames, tab, st);
+    else xa_launch<B, true, kInCU8, 0>(in, n, lo, out, frames, tab, st);
+  }
+  return hipGetLastError();
 }
 
 }  // namespace xa
 
-#ifndef XA_STAMPS
-#define XA_STAMPS 0
-#endif
 // Debug hook (not part of zfft.h): copies and clears the stamp sums of a XA_STAMPS build
 // (segment cycles summed over waves, then the tile count); -1 in a normal build.
 extern "C" int zfft_debug_xa_stamps(unsigned long long *out) {
@@ -880,24 +813,7 @@ extern "C" int zfft_debug_xa_stamps(unsigned long long *out) {
 
 hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix, float2 *out,
                            int frames, const XaTab *tab, hipStream_t st) {
-  using namespace xa;
-  if (!mix) {
-    if (in.dtype != kInC64 || in.flip) return hipErrorInvalidValue;  // stages >= 1: internal
-    xa_launch<false, kInC64, 0>(in, n, lo, out, frames, tab, st);
-  } else if (in.dtype == kInC64) {
-    if (in.flip) xa_launch<true, kInC64, 1>(in, n, lo, out, frames, tab, st);
-    else xa_launch<true, kInC64, 0>(in, n, lo, out, frames, tab, st);
-  } else if (in.dtype == kInC32H) {
-    if (in.flip) xa_launch<true, kInC32H, 1>(in, n, lo, out, frames, tab, st);
-    else xa_launch<true, kInC32H, 0>(in, n, lo, out, frames, tab, st);
-  } else if (in.dtype == kInF32R) {
-    if (in.flip) xa_launch<true, kInF32R, 1>(in, n, lo, out, frames, tab, st);
-    else xa_launch<true, kInF32R, 0>(in, n, lo, out, frames, tab, st);
-  } else {
-    if (in.flip) xa_launch<true, kInCU8, 1>(in, n, lo, out, frames, tab, st);
-    else xa_launch<true, kInCU8, 0>(in, n, lo, out, frames, tab, st);
-  }
-  return hipGetLastError();
+  return xa::xa_dispatch<kXaB>(in, n, lo, mix, out, frames, tab, st);
 }
 
 }  // namespace zfft

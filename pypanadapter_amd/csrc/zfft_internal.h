@@ -78,18 +78,19 @@ hipError_t launch_fused_pass(const float2 *in, float2 *out, bool desc, bool two,
 // positions, and a backward all-pole cascade 1/D2(w), D2(z^2) = D(z) D(-z), at the output
 // rate: 8 + 12.5 + 4 multiply-adds per input sample instead of 2 x 17 for two DF2T passes,
 // with scipy's pad / steady-state edge rules carried over exactly.  One wave per frame,
-// tiles of 64 lanes x kXaB samples, states scanned over lanes in the real modal basis of
-// each all-pole cascade (sections slowest pole first, the lower-error order in fp32).
-constexpr int kXaB = 32;             // forward samples per lane and tile
-constexpr int kXaT = 64 * kXaB;      // tile (forward samples)
-constexpr int kXaK = kXaB / 2;       // kept outputs per lane and tile
+// tiles of 64 lanes x B samples (B = 32 or 64), states scanned over lanes in the real modal
+// basis of each all-pole cascade (sections slowest pole first, the lower-error fp32 order).
 constexpr int kXaLag = 192;          // held-tile outputs corrected by the one-tile lag
-// scan levels per mode (modes follow the cascade order, slowest pole first): mode j needs
-// |lambda_j|^(S 2^levels) < 1e-9; checked when the tables are built.  Modes 0, 1 scan
-// inside 16-lane rows (DPP row shifts, <= 4 levels) and then add the adjacent row's end
-// lane; modes 2, 3 take one whole-wave shift (1 level).
-constexpr int kXaLevels[4] = {4, 2, 1, 1};
-constexpr int kXaRowModes = 2;
+constexpr int kXaB = 32;             // lane sub-block: samples per lane and tile
+constexpr int kXaRowModes = 2;       // modes scanned inside 16-lane DPP rows (+ one cross-row step)
+// Scan levels of mode j for lane sub-blocks of B forward samples (B/2 backward): mode j
+// needs |lambda_j|^(S 2^levels) < 1e-9 (radii .935 .808 .682 .587, the backward poles
+// squared at half the steps); checked when the tables are built.  Modes 0, 1 scan inside
+// 16-lane rows (DPP row shifts, <= 4 levels) and then add the adjacent row's end lane;
+// modes 2, 3 take one whole-wave shift (1 level).
+__host__ __device__ constexpr int xa_levels(int B, int j) {
+  return B == 32 ? (j == 0 ? 4 : j == 1 ? 2 : 1) : (j == 0 ? 3 : 1);
+}
 struct XaPass {                      // one all-pole cascade, DF-I state (y[t-1], y[t-2]) per section
   float a1[4], a2[4];                // y = x - a1 y[t-1] - a2 y[t-2], cascade order
   float ti[8][8];                    // T^-1: state -> real modal (block lower triangular)
@@ -102,7 +103,7 @@ struct XaPass {                      // one all-pole cascade, DF-I state (y[t-1]
   alignas(16) float xr[16][4];
 };
 struct XaTab {
-  XaPass f, b;                       // forward (full rate, S = kXaB), backward (S = kXaK)
+  XaPass f, b;                       // forward (full rate, S = B), backward (S = B/2)
   float m25[25];                     // M on v[j-8 .. j+16]
   float mp17[17];                    // N(1/z) D(-1/z) on f[j .. j+16] (frame-end form)
   float n9[9];                       // N on v[s .. s-8] (f = N v, frame-end form)
@@ -110,6 +111,12 @@ struct XaTab {
   float vss;                         // forward cascade output per unit constant input
   float pad_[2];
   alignas(16) float lag[kXaLag][8];  // backward C A2^d T: held output d steps below the top
+  // forward zero-input responses (the exact entering state's part, added after the zero-state
+  // pass instead of a second pass): C A^t T for the B own samples, and their images through
+  // the FIR -- on this lane's K outputs (gown) and on its share of the next lane's 12 (gnb)
+  alignas(16) float fcat[kXaB][8];
+  alignas(16) float gown[kXaB / 2][8];
+  alignas(16) float gnb[12][8];
 };
 
 hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix,

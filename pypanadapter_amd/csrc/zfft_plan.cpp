@@ -141,7 +141,8 @@ void modal_basis(const Mat8 &A, const cd lam[4], Mat8 &T) {
 
 // One pass: fills P, the output table cm (steps rows) and, when lag != nullptr, the
 // far-field rows C A^d T for d < n_lag.
-bool xa_pass_tables(const ApD &c, int steps, bool up, XaPass &P, float (*lag)[8], int n_lag) {
+bool xa_pass_tables(const ApD &c, int steps, bool up, XaPass &P, float (*lag)[8], int n_lag, int B,
+                    double (*lag_d)[8] = nullptr) {
   Mat8 A(64);
   double C[8];
   for (int q = 0; q < 8; ++q) {
@@ -174,7 +175,7 @@ bool xa_pass_tables(const ApD &c, int steps, bool up, XaPass &P, float (*lag)[8]
   }
   for (int j = 0; j < 4; ++j) {
     // the kernel's truncated scan must reach fp32-negligible powers for every mode
-    if (std::pow(std::abs(lam[j]), (double)(steps << kXaLevels[j])) > 1e-9) return false;
+    if (std::pow(std::abs(lam[j]), (double)(steps << xa_levels(B, j))) > 1e-9) return false;
     const cd w = std::pow(lam[j], steps);
     P.pS[j][0] = (float)w.real();
     P.pS[j][1] = (float)w.imag();
@@ -187,7 +188,7 @@ bool xa_pass_tables(const ApD &c, int steps, bool up, XaPass &P, float (*lag)[8]
   for (int i = 0; i < 16; ++i)
     for (int j = 0; j < 4; ++j) P.xr[i][j] = 0.f;
   for (int j = 0; j < kXaRowModes; ++j) {
-    if (kXaLevels[j] > 4) return false;  // row shifts reach at most 8 lanes
+    if (xa_levels(B, j) > 4) return false;  // row shifts reach at most 8 lanes
     for (int i = 0; i < 16; ++i) {
       const cd u = std::pow(lam[j], steps * (up ? i + 1 : 16 - i));
       P.xr[i][2 * j] = (float)u.real();
@@ -200,13 +201,14 @@ bool xa_pass_tables(const ApD &c, int steps, bool up, XaPass &P, float (*lag)[8]
       double acc = 0;
       for (int r = 0; r < 8; ++r) acc += C[r] * AtT[r * 8 + q];
       lag[t][q] = (float)acc;
+      if (lag_d) lag_d[t][q] = acc;
     }
     AtT = matmul8(A, AtT);
   }
   return true;
 }
 
-bool xa_build_tables(XaTab &X) {
+bool xa_build_tables(XaTab &X, int B) {
   // sections slowest pole first (the lower-error fp32 order; any order is exact)
   ApD fw, bw;
   for (int k = 0; k < 4; ++k) {
@@ -216,8 +218,10 @@ bool xa_build_tables(XaTab &X) {
     bw.a1[k] = 2.0 * a2 - a1 * a1;  // D(z) D(-z) = D2(z^2)
     bw.a2[k] = a2 * a2;
   }
-  if (!xa_pass_tables(fw, kXaB, true, X.f, nullptr, 0) ||
-      !xa_pass_tables(bw, kXaK, false, X.b, X.lag, kXaLag))
+  if (B != kXaB) return false;
+  static double fcat[kXaB][8];
+  if (!xa_pass_tables(fw, B, true, X.f, X.fcat, B, B, fcat) ||
+      !xa_pass_tables(bw, B / 2, false, X.b, X.lag, kXaLag, B))
     return false;
   // N = b0 (1 + z^-1)^8 (sections 1..3 are exactly [1, 2, 1], section 0 is b0 [1, 2, 1])
   double n9[9], dneg[9] = {1.0}, mp[17] = {0}, m25[25] = {0};
@@ -249,6 +253,27 @@ bool xa_build_tables(XaTab &X) {
     mps += mp[t];
   }
   for (int u = 0; u < 25; ++u) X.m25[u] = (float)m25[u];
+  // the zero-input responses through the FIR (xa_kernels.hip): output k of a lane takes
+  // taps m25[24 + t - 1 - 2k] on its own v[t]; its share of the next lane's output k takes
+  // m25[t - (B - 24) - 1 - 2k] on its v[t], t >= B - 23
+  for (int k = 0; k < B / 2; ++k)
+    for (int r = 0; r < 8; ++r) {
+      double g = 0;
+      for (int t = 0; t < B; ++t) {
+        const int tap = 24 + t - 1 - 2 * k;
+        if (tap >= 0 && tap < 25) g += m25[tap] * fcat[t][r];
+      }
+      X.gown[k][r] = (float)g;
+    }
+  for (int k = 0; k < 12; ++k)
+    for (int r = 0; r < 8; ++r) {
+      double g = 0;
+      for (int t = B - 23; t < B; ++t) {
+        const int tap = t - (B - 24) - 1 - 2 * k;
+        if (tap >= 0 && tap < 25) g += m25[tap] * fcat[t][r];
+      }
+      X.gnb[k][r] = (float)g;
+    }
   for (int i = 0; i < 9; ++i) X.n9[i] = (float)n9[i];
   for (int k = 0; k < 4; ++k) vss /= 1.0 + fw.a1[k] + fw.a2[k];
   X.mp_sum = (float)mps;
@@ -429,7 +454,7 @@ int ensure_lo(zfft_plan *p, int64_t L) {
   if (p->lo_len >= L) return ZFFT_OK;
   int rc = quiesce(p);
   if (rc) return rc;
-  int64_t cap = L;
+  int64_t cap = std::max<int64_t>(L, 64);  // the XA kernels read lo[lane] for every lane
   std::vector<float2> h(cap);
   const double r = p->cfg.f_lo / p->cfg.fs, sq2 = std::sqrt(2.0);
   for (int64_t n = 0; n < cap; ++n) {
@@ -888,14 +913,14 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
       e = hipMemcpy(p->tws.p, ts.data(), ts.size() * sizeof(float2), hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) {
-    static XaTab xa{};
-    static const bool xa_ok = xa_build_tables(xa);
+    static XaTab xa[1]{};
+    static const bool xa_ok = xa_build_tables(xa[0], kXaB);
     if (!xa_ok) {
       zfft_plan_destroy(p);
       return fail(ZFFT_EHIP, "XA tables: scan levels too shallow for the filter poles");
     }
-    e = p->xa_tab.ensure(sizeof(XaTab));
-    if (e == hipSuccess) e = hipMemcpy(p->xa_tab.p, &xa, sizeof(XaTab), hipMemcpyHostToDevice);
+    e = p->xa_tab.ensure(sizeof(xa));
+    if (e == hipSuccess) e = hipMemcpy(p->xa_tab.p, xa, sizeof(xa), hipMemcpyHostToDevice);
   }
   if (e != hipSuccess) {
     zfft_plan_destroy(p);
