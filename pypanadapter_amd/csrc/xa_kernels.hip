@@ -50,8 +50,12 @@
 namespace zfft {
 namespace xa {
 
-constexpr int kHalfRows = 32;           // transposes go through LDS one half tile at a time
-constexpr int kWaves = 2;               // waves (frames) per workgroup
+// Tiles go in and out through LDS transposes with both halves (32 lanes' rows each) held at
+// once: one LDS round trip per direction and tile (two halves in turn: 4 % slower at cfg2).
+// 4-wave workgroups: 2 of them (78 KB of LDS each) fill a CU at 2 waves per SIMD.
+constexpr int kHalfRows = 32;           // rows of one transpose half (32 lanes' sub-blocks)
+constexpr int kHalves = 2;              // transpose halves held in LDS at once
+constexpr int kWaves = 4;               // waves (frames) per workgroup
 constexpr int kLagChunks = kXaLag / 64; // held output chunks of a tile
 
 template <int B>
@@ -64,7 +68,7 @@ struct Geo {
   static constexpr int kRowsPerChunk = 64 / B > 0 ? 64 / B : 1;  // input rows one 64-sample chunk fills
   // LDS per wave: half-tile transposes + FIR carry (12 used) + frame-end v carry (the 64 v
   // before the last tile) + LO chunk starts (B)
-  static constexpr int kBuf = kHalfRows * kRow + 16 + 64 + B;
+  static constexpr int kBuf = kHalves * kHalfRows * kRow + 16 + 64 + B;
   static constexpr int kWavesPerSimd = B == 32 ? 2 : 1;  // the register budget is cut for
 };
 
@@ -325,7 +329,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   if (f >= frames) return;  // whole wave
   const LP buf0 = (LP)lds_all[wv];           // half-tile transposes: 32 rows of kRow v2f
   LP buf = buf0;
-  LP pcarry = buf + kHalfRows * kRow;       // lane 63's FIR neighbour part, for next lane 0
+  LP pcarry = buf + kHalves * kHalfRows * kRow;  // lane 63's FIR neighbour part, for next lane 0
   LP vcarry = pcarry + 16;                  // the 64 v before the last tile
   LP cq = vcarry + 64;                      // lo at the B chunk starts of the tile
   const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
@@ -371,39 +375,28 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     const int m0 = m_of(tile, ln);
     v2f *__restrict__ od = o + m0;
     const bool inside = m_of(tile, 0) >= 0 && m_of(tile, T / 2) <= n_out;  // wave-uniform
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      if ((ln >> 5) == hf) {  // lanes of this half: K outputs each into row ln % 32
-        LP4 hw = (LP4)(buf + (ln & 31) * kHeldRow);
+    {  // every lane's K outputs into row ln, one LDS round trip
+      {
+        LP4 hw = (LP4)(buf + ln * kHeldRow);
 #pragma unroll
         for (int k = 0; k < K / 2; ++k) hw[k] = v4f{h[2 * k].x, h[2 * k].y, h[2 * k + 1].x, h[2 * k + 1].y};
       }
       __builtin_amdgcn_wave_barrier();
-      // output idx = 64 c + ln (c in this half) sits at row idx/K - 32 hf, column idx % K;
-      // all the half's chunks are read first (one LDS round trip), then stored: an interior
-      // tile (wave-uniform `inside`) stores without per-chunk tests
+      // output idx = 64 c + ln sits at row idx/K, column idx % K
       const LP hr = buf + (ln / K) * kHeldRow + (ln % K);
-      v2f vc[kChunks / 2];
+      v2f vc[kChunks];
 #pragma unroll
-      for (int cc = 0; cc < kChunks / 2; ++cc) vc[cc] = hr[cc * (64 / K) * kHeldRow];
+      for (int c = 0; c < kChunks; ++c) vc[c] = hr[c * (64 / K) * kHeldRow];
       if (inside) {
 #pragma unroll
-        for (int cc = 0; cc < kChunks / 2; ++cc) {
-          const int c = hf * (kChunks / 2) + cc;
-          if (c < kChunks - kLagChunks) od[64 * c] = vc[cc];
-        }
+        for (int c = 0; c < kChunks - kLagChunks; ++c) od[64 * c] = vc[c];
       } else {
 #pragma unroll
-        for (int cc = 0; cc < kChunks / 2; ++cc) {
-          const int c = hf * (kChunks / 2) + cc;
-          if (c < kChunks - kLagChunks && m0 + 64 * c >= 0 && m0 + 64 * c < n_out) od[64 * c] = vc[cc];
-        }
+        for (int c = 0; c < kChunks - kLagChunks; ++c)
+          if (m0 + 64 * c >= 0 && m0 + 64 * c < n_out) od[64 * c] = vc[c];
       }
 #pragma unroll
-      for (int cc = 0; cc < kChunks / 2; ++cc) {
-        const int c = hf * (kChunks / 2) + cc;
-        if (c >= kChunks - kLagChunks) held[c - (kChunks - kLagChunks)] = vc[cc];
-      }
+      for (int c = kChunks - kLagChunks; c < kChunks; ++c) held[c - (kChunks - kLagChunks)] = vc[c];
       __builtin_amdgcn_wave_barrier();
     }
   };
@@ -477,7 +470,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       LP b = buf0;
       asm volatile("" : "+s"(b));
       buf = b;
-      pcarry = buf + kHalfRows * kRow;
+      pcarry = buf + kHalves * kHalfRows * kRow;
       vcarry = pcarry + 16;
       cq = vcarry + 64;
     }
@@ -487,21 +480,19 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     {
       const bool fast = fast_tile(base);  // wave-uniform
       LP st = buf + (ln / B) * kRow + (ln % B);
-      auto read_rows = [&](int hf) {  // lanes of half hf take their rows
+      // the fast and the edge path are separate blocks end to end: raw registers of the
+      // fast path never live across the edge path's code (which would force their spill)
+      auto read_all_rows = [&]() {  // every lane its row (half ln / 32), both halves at once
         __builtin_amdgcn_wave_barrier();
-        if ((ln >> 5) == hf) {
-          const LP4 rp = (LP4)(buf + (ln & 31) * kRow);
+        const LP4 rp = (LP4)(buf + (ln >> 5) * (kHalfRows * kRow) + (ln & 31) * kRow);
 #pragma unroll
-          for (int t = 0; t < B / 2; ++t) {
-            const v4f w = rp[t];
-            y[2 * t] = v2f{w.x, w.y};
-            y[2 * t + 1] = v2f{w.z, w.w};
-          }
+        for (int t = 0; t < B / 2; ++t) {
+          const v4f w = rp[t];
+          y[2 * t] = v2f{w.x, w.y};
+          y[2 * t + 1] = v2f{w.z, w.w};
         }
         __builtin_amdgcn_wave_barrier();
       };
-      // the fast and the edge path are separate blocks end to end: raw registers of the
-      // fast path never live across the edge path's code (which would force their spill)
       if (fast) {
         if (MIX) {
           if (ln < B) cq[ln] = cqv;
@@ -514,17 +505,18 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
             const int q = hf * (B / 2) + qq;
             v2f x = cvt_raw<DT>(pf[q]);
             if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl));
-            st[G::kRowsPerChunk * kRow * qq] = x;
+            st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = x;
           }
-          read_rows(hf);
         }
+        read_all_rows();
       } else {
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll 4
-          for (int qq = 0; qq < B / 2; ++qq) st[G::kRowsPerChunk * kRow * qq] = ext(base + ln + 64 * (hf * (B / 2) + qq));
-          read_rows(hf);
+          for (int qq = 0; qq < B / 2; ++qq)
+            st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = ext(base + ln + 64 * (hf * (B / 2) + qq));
         }
+        read_all_rows();
       }
     }
     next_fast = tau + 1 < nt && fast_tile(base + T);  // wave-uniform
