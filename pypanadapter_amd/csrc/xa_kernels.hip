@@ -50,9 +50,6 @@
 namespace zfft {
 namespace xa {
 
-#ifndef XA_PF_EARLY
-#define XA_PF_EARLY 0  // every next-tile load issued at the tile start
-#endif
 // Tiles go in and out through LDS transposes with both halves (32 lanes' rows each) held at
 // once: one LDS round trip per direction and tile (two halves in turn: 4 % slower at cfg2).
 // 4-wave workgroups: 2 of them (78 KB of LDS each) fill a CU at 2 waves per SIMD.
@@ -529,17 +526,12 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       next_off = (uint32_t)((FLIP ? in.len - 1 - i0 : (int64_t)i0) * (int64_t)sizeof(RawT));
     }
     // the next tile's loads: groups 0-3 now, 4-5 after the forward pass, 6-7 after the scan
-    // (later issue points leave the register allocator room it does not use: spills)
+    // (later issue points leave the register allocator room it does not use: spills; all
+    // eight groups at the tile start measured no faster)
     issue_group(0);
     issue_group(1);
     issue_group(2);
     issue_group(3);
-    if (XA_PF_EARLY) {
-      issue_group(4);
-      issue_group(5);
-      issue_group(6);
-      issue_group(7);
-    }
     XA_STAMP(0);
 
     // ---- forward all-pole cascade: one pass from a zero state streaming the FIR (v0 -> h
@@ -608,10 +600,8 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
           }
         }
         XA_STAMP(1);
-        if (!XA_PF_EARLY) {
-          issue_group(4);
-          issue_group(5);
-        }
+        issue_group(4);
+        issue_group(5);
         fold_entering<0>(m, m_in, tab, ln == 0);
         modal_scan<B, 0, true>(m, tab, ln, xw_l[0][ln & 15]);
 #pragma unroll
@@ -620,10 +610,8 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
         for (int r = 0; r < 8; ++r) m_in.r[r] = lane_of(m.r[r], 63);  // next tile's entering state
       }
       XA_STAMP(2);
-      if (!XA_PF_EARLY) {
-        issue_group(6);
-        issue_group(7);
-      }
+      issue_group(6);
+      issue_group(7);
       // + the entering state's response through the FIR (own outputs, neighbour share);
       // row k's constants are read once output k-4 is done (at most 4 rows in flight)
       // (scalar reads; row k once output k-4 is done: LDS broadcast reads measured 6 % slower)
