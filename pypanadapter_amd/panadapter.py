@@ -52,18 +52,21 @@ class PlanCache:
         return self.plan
 
 
-def _cache(device: int) -> PlanCache:
+def _cache(device: int, purpose: str = "rows") -> PlanCache:
+    """Per thread, device and purpose: zoomfft and psd_row keep separate plans, so code
+    alternating the two does not rebuild a plan on every call."""
     caches = getattr(_tls, "caches", None)
     if caches is None:
         caches = _tls.caches = {}
-    if device not in caches:
-        caches[device] = PlanCache(device)
-    return caches[device]
+    key = (device, purpose)
+    if key not in caches:
+        caches[key] = PlanCache(device)
+    return caches[key]
 
 
 def zoomfft(x, ratio: int, fs: float, f_lo: float = 1.0, device: int = 0) -> np.ndarray:
     """ApplicationDisplay.zoomfft (S:2088-2100): LO mix + log2(ratio) x decimate(x, 2)."""
-    plan = _cache(device).get(fs, 32, int(ratio), 2, "hamming", f_lo)
+    plan = _cache(device, "zoomfft").get(fs, 32, int(ratio), 2, "hamming", f_lo)
     return plan.decimate(x)
 
 
