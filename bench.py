@@ -27,6 +27,7 @@ process pool of the job's CPU share, run BEFORE the GPU is touched.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import math
 import os
@@ -163,6 +164,19 @@ def spawn_ranks(argv) -> int:
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
+    # a rank that fails ends the others (which would wait in the barrier for it)
+    while any(p.poll() is None for p in procs):
+        if any(p.returncode not in (None, 0) for p in procs):
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
     return max(abs(p.wait()) for p in procs)
 
 
@@ -321,7 +335,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist  # gloo on the host: barrier + max-reduce only
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=600))
+    if args.dry_run and os.environ.get("BENCH_DRY_RUN_FAIL_RANK") == str(rank):
+        sys.exit(3)  # launcher test: a rank that dies before the barrier
     if args.dry_run:  # the launcher's contract without touching a GPU
         me = torch.tensor([rank, local, world, os.getpid()], dtype=torch.int64)
         allr = [torch.zeros(4, dtype=torch.int64) for _ in range(world)] if dist else [me]

@@ -599,11 +599,8 @@ __device__ __forceinline__ int stockham_out_index(int t, int N, int Ns, int i) {
 // pass; then radix-16 Stockham passes through LDS; the last pass accumulates |X|^2 in
 // registers for every bin the thread owns.  The next segment's loads are issued before
 // the current FFT (register prefetch).  Finally: density scale, fftshift crop, 20 log10.
-#ifndef WELCH_MINB
-#define WELCH_MINB 1
-#endif
 template <int R0, bool PF, int MAXT>  // PF: register prefetch of the next segment
-__global__ __launch_bounds__(MAXT, (MAXT == 256 ? WELCH_MINB : 1)) void welch_rows_kernel(const v2f *__restrict__ x, int64_t len,
+__global__ __launch_bounds__(MAXT, 1) void welch_rows_kernel(const v2f *__restrict__ x, int64_t len,
                                                           const float *__restrict__ win,
                                                           const v2f *__restrict__ tw,
                                                           WelchGeom g, float *__restrict__ rows,
@@ -718,24 +715,14 @@ __global__ __launch_bounds__(MAXT, (MAXT == 256 ? WELCH_MINB : 1)) void welch_ro
 // per segment from four powers per stage (w, w^2, w^4, w^8; at most three products deep).
 // PRUNE (W <= 2N/RL): the fftshift crop keeps only last-stage outputs 0 and RL-1, so the
 // last stage forms just those two per block.
-#ifndef WELCH_DIF_PF
-#define WELCH_DIF_PF 16  // values per thread prefetched a segment ahead (N = 4096)
-#endif
-#ifndef WELCH_DIF_PF_SMALL
-#define WELCH_DIF_PF_SMALL 8  // the same for N <= 2048
-#endif
-#ifndef WELCH_DIF_WAVES
-#define WELCH_DIF_WAVES 3  // waves per SIMD the registers are cut for (PRUNE, N = 4096)
-#endif
-#ifndef WELCH_DIF_WAVES_SMALL
-#define WELCH_DIF_WAVES_SMALL 3  // the same for N <= 2048 (full form)
-#endif
-#ifndef WELCH_DIF_WAVES_SMALL_PRUNE
-#define WELCH_DIF_WAVES_SMALL_PRUNE 4  // N <= 2048, PRUNE: 4 waves/SIMD (cfg1: 4096 one-wave
-#endif                                 // frames fill the GPU's 4096 slots in one round)
-#ifndef WELCH_DIF_PF_SMALL_PRUNE
-#define WELCH_DIF_PF_SMALL_PRUNE 4  // prefetch of that form (fits 128 VGPRs)
-#endif
+// Register plans (measured on MI355X):
+constexpr int kDifPf = 16;             // values per thread prefetched a segment ahead (N = 4096)
+constexpr int kDifPfSmall = 8;         // the same for N <= 2048
+constexpr int kDifWaves = 3;           // waves per SIMD the registers are cut for (PRUNE, N = 4096)
+constexpr int kDifWavesSmall = 3;      // the same for N <= 2048 (full form)
+constexpr int kDifWavesSmallPrune = 4; // N <= 2048, PRUNE: 4 waves/SIMD (cfg1: 4096 one-wave
+                                       // frames fill the GPU's 4096 slots in one round)
+constexpr int kDifPfSmallPrune = 4;    // prefetch of that form (fits 128 VGPRs)
 __host__ __device__ constexpr int dif_slot(int i) { return i + (i >> 4); }  // conflict-free strides 1, 16, 17
 
 template <int N>
@@ -750,11 +737,11 @@ struct Dif {
   static constexpr int NT = T * FPB;                 // threads per workgroup
   static constexpr int NW = (T + 63) / 64;           // waves per frame
   static constexpr int SLOTS = dif_slot(N - 1) + 1;  // LDS image per frame (v2f)
-  static constexpr int PF = N <= 2048 ? WELCH_DIF_PF_SMALL : WELCH_DIF_PF;
-  static constexpr int PF_PRUNE = N <= 2048 ? WELCH_DIF_PF_SMALL_PRUNE : WELCH_DIF_PF;
+  static constexpr int PF = N <= 2048 ? kDifPfSmall : kDifPf;
+  static constexpr int PF_PRUNE = N <= 2048 ? kDifPfSmallPrune : kDifPf;
   // waves per SIMD the registers are cut for
-  static constexpr int WAVES_PRUNE = N <= 2048 ? WELCH_DIF_WAVES_SMALL_PRUNE : N == 4096 ? WELCH_DIF_WAVES : 2;
-  static constexpr int WAVES_FULL = N <= 2048 ? WELCH_DIF_WAVES_SMALL : 2;
+  static constexpr int WAVES_PRUNE = N <= 2048 ? kDifWavesSmallPrune : N == 4096 ? kDifWaves : 2;
+  static constexpr int WAVES_FULL = N <= 2048 ? kDifWavesSmall : 2;
 };
 
 // bin of slot q after the last stage (digits reversed)
@@ -1283,19 +1270,13 @@ static hipError_t welch_launch_t(const float2 *x, int64_t len, const float *win,
   return hipGetLastError();
 }
 
-#ifndef WELCH_DIF
-#define WELCH_DIF 1
-#endif
-#ifndef WELCH_DIF_MIN
-#define WELCH_DIF_MIN 1024
-#endif
-#ifndef WELCH_DIF_MAX
-#define WELCH_DIF_MAX 8192  // (N = 16384 as one 1024-thread frame spills: four-step by default)
-#endif
+// the in-place DIF kernel covers 1024 <= N <= 8192 (N = 16384 as one 1024-thread frame
+// spills: four-step by default there)
+constexpr int kDifMin = 1024, kDifMax = 8192;
 template <int R0>
 static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
                                const WelchGeom &g, float *rows, int frames, hipStream_t st) {
-  if (WELCH_DIF && g.nperseg == g.n_fft && g.n_fft >= WELCH_DIF_MIN && g.n_fft <= WELCH_DIF_MAX) {
+  if (g.nperseg == g.n_fft && g.n_fft >= kDifMin && g.n_fft <= kDifMax) {
     switch (g.n_fft) {
       case 1024: return welch_dif_launch<1024>(x, len, win, tw, g, rows, frames, st);
       case 2048: return welch_dif_launch<2048>(x, len, win, tw, g, rows, frames, st);
@@ -1305,10 +1286,7 @@ static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, c
     }
   }
   // threads = N/16 (>= 64): N <= 4096 -> <= 256 threads, room for the prefetch registers
-#ifndef WELCH_PF
-#define WELCH_PF 1
-#endif
-  if (g.n_fft <= 4096) return welch_launch_t<R0, WELCH_PF != 0, 256>(x, len, win, tw, g, rows, frames, st);
+  if (g.n_fft <= 4096) return welch_launch_t<R0, true, 256>(x, len, win, tw, g, rows, frames, st);
   if (g.n_fft <= 8192) return welch_launch_t<R0, false, 512>(x, len, win, tw, g, rows, frames, st);
   return welch_launch_t<R0, false, 1024>(x, len, win, tw, g, rows, frames, st);
 }

@@ -43,3 +43,15 @@ def test_torchrun_environment_is_honoured():
     assert len(lines) == 1
     res = json.loads(lines[0])
     assert res["world"] == 2 and sorted(r["local_rank"] for r in res["ranks"]) == [0, 1]
+
+
+def test_failed_rank_ends_the_others():
+    """A rank that dies before the barrier must not leave the others waiting in it: the
+    launcher ends them and returns the failure."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["BENCH_DRY_RUN_FAIL_RANK"] = "1"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3",
+                          "--dry-run", "--no-cpu"], capture_output=True, text=True, timeout=240,
+                         env=env, cwd=ROOT)
+    assert out.returncode != 0
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
