@@ -40,11 +40,15 @@
 // Numerics: float32, max relative error ~8e-6 of the decimated IQ vs float64 sosfiltfilt
 // (plain float32 sosfiltfilt: ~1e-6); end-to-end rows within 1e-5 dB (tools/xa_proto.py).
 #include <cstddef>
+#include <type_traits>
 
 #include "zfft_device.h"
 
 #ifndef XA_STAMPS
 #define XA_STAMPS 0
+#endif
+#ifndef XA_WIDE
+#define XA_WIDE 1  // tile loads and output stores two elements per lane (0: one)
 #endif
 
 namespace zfft {
@@ -73,6 +77,7 @@ struct Geo {
 };
 
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 // LDS pointers keep their address space (a generic pointer turns every LDS access into a
 // flat access, which waits on vector memory too)
 typedef v2f __attribute__((address_space(3))) *LP;
@@ -102,11 +107,20 @@ __device__ __forceinline__ v2f cvt_raw(typename Raw<DT>::T r) {  // as load_in_t
   else return v2f{((float)r.x - 127.5f) * (1.f / 127.5f), ((float)r.y - 127.5f) * (1.f / 127.5f)};
 }
 
-// one raw element through a buffer resource (out-of-range offsets read 0)
+// Two consecutive raw elements: the wide tile loads take a pair per lane (16 B for
+// complex64: the gfx950 memory path moves 16-B lanes at a better rate than 8-B ones).
+template <int DT> struct Pair {
+  typename Raw<DT>::T a, b;
+};
+
+// one raw element (or pair) through a buffer resource (out-of-range offsets read 0)
 template <class T>
 __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   T v;
-  if constexpr (sizeof(T) == 8) {
+  if constexpr (sizeof(T) == 16) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    __builtin_memcpy(&v, &u, 16);
+  } else if constexpr (sizeof(T) == 8) {
     const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
     __builtin_memcpy(&v, &u, 8);
   } else if constexpr (sizeof(T) == 4) {
@@ -335,6 +349,8 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
   const int nt = (e + 15) / T + 1;  // the last FIR/backward tile reaches e - 1
   v2f *__restrict__ o = out + (int64_t)f * n_out;
+  const __amdgpu_buffer_rsrc_t orsrc =  // the frame's output row (wide stores)
+      __builtin_amdgcn_make_buffer_rsrc((void *)o, (short)0, n_out * 8, 0x00020000);
   auto X = [&](int i) -> v2f {
     v2f v = load_in_t<DT, FLIP>(in, f, i);
     if constexpr (MIX) v = cmul(v, lo[i]);
@@ -385,14 +401,33 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       // output idx = 64 c + ln sits at row idx/K, column idx % K
       const LP hr = buf + (ln / K) * kHeldRow + (ln % K);
       v2f vc[kChunks];
+      // wide: the final outputs 0 .. 128 nw - 1 as pairs (128 C + 2 ln + {0, 1}: row 8 C +
+      // ln/8, cols 2 (ln%8) + {0, 1}; one b128 read, one 16-B store), the rest one per lane
+      constexpr int nw = XA_WIDE ? (kChunks - kLagChunks) / 2 : 0;
+      v4f vw[nw > 0 ? nw : 1];
+      if constexpr (nw > 0) {
+        const LP4 hr2 = (LP4)(buf + (ln / 8) * kHeldRow + 2 * (ln % 8));
 #pragma unroll
-      for (int c = 0; c < kChunks; ++c) vc[c] = hr[c * (64 / K) * kHeldRow];
+        for (int c = 0; c < nw; ++c) vw[c] = hr2[c * (8 * kHeldRow / 2)];
+      }
+#pragma unroll
+      for (int c = 2 * nw; c < kChunks; ++c) vc[c] = hr[c * (64 / K) * kHeldRow];
       if (inside) {
 #pragma unroll
-        for (int c = 0; c < kChunks - kLagChunks; ++c) od[64 * c] = vc[c];
+        for (int c = 0; c < nw; ++c)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vw[c]), orsrc,
+                                                 (uint32_t)(m_of(tile, 128 * c + 2 * ln) * 8), 0, 0);
+#pragma unroll
+        for (int c = 2 * nw; c < kChunks - kLagChunks; ++c) od[64 * c] = vc[c];
       } else {
 #pragma unroll
-        for (int c = 0; c < kChunks - kLagChunks; ++c)
+        for (int c = 0; c < nw; ++c) {
+          const int m = m_of(tile, 128 * c + 2 * ln);
+          if (m >= 0 && m < n_out) o[m] = v2f{vw[c].x, vw[c].y};
+          if (m + 1 >= 0 && m + 1 < n_out) o[m + 1] = v2f{vw[c].z, vw[c].w};
+        }
+#pragma unroll
+        for (int c = 2 * nw; c < kChunks - kLagChunks; ++c)
           if (m0 + 64 * c >= 0 && m0 + 64 * c < n_out) od[64 * c] = vc[c];
       }
 #pragma unroll
@@ -440,21 +475,32 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   typedef typename Raw<DT>::T RawT;
   const RawT *__restrict__ src = (const RawT *)in.p + (int64_t)f * in.stride;
   auto fast_tile = [&](int b) { return b >= kPad && b + T <= n + kPad; };
-  v2f wl = splat(0.f);  // lo[n0 + l] = lo[n0] w^l: w^l = lo[l] / sqrt(2), per lane
-  if constexpr (MIX) wl = lo[lane] * 0.70710678118654752f;
-  v2f cqv = splat(0.f);  // lo[next tile start - 27 + 64 (lane % B)], loaded a tile ahead
-  RawT pf[B];            // the next tile's B input chunks
+  // narrow (XA_WIDE 0): chunk q = samples 64 q + lane; wide: chunk q = samples 128 q +
+  // 2 lane + {0, 1}, a pair per lane -- half the load (and LDS write) instructions
+  constexpr int kPer = XA_WIDE ? 2 : 1;  // elements per lane and chunk
+  constexpr int kCh = B / kPer;          // input chunks per tile
+  constexpr int kSpan = 64 * kPer;       // samples per chunk
+  typedef typename std::conditional<XA_WIDE, Pair<DT>, RawT>::type LoadT;
+  // lo[n0 + l] = lo[n0] lo[l] / sqrt(2): the chunk start times a per-lane factor (one per
+  // element of the lane); lo has >= 2048 entries whenever a fast tile exists (L > 2048)
+  v2f wl0 = splat(0.f), wl1 = splat(0.f);
+  if constexpr (MIX) {
+    wl0 = lo[min(kPer * lane, n - 1)] * 0.70710678118654752f;
+    wl1 = lo[min(kPer * lane + 1, n - 1)] * 0.70710678118654752f;
+  }
+  v2f cqv = splat(0.f);  // lo[next tile start - 27 + kSpan (lane % kCh)], loaded a tile ahead
+  LoadT pf[kCh];         // the next tile's input chunks
   bool next_fast = false;
   int next_i0 = 0;  // first input index of the next tile
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void *)src, (short)0, (int)(in.len * (int64_t)sizeof(RawT)), 0x00020000);
-  uint32_t next_off = 0;  // byte offset of this lane's element of the next tile's chunk 0
-  // next-tile loads: group g = chunks [g B/8, (g+1) B/8), issued at 8 points of the tile
+  uint32_t next_off = 0;  // byte offset of this lane's (first) element of the next tile's chunk 0
+  // next-tile loads: group g = chunks [g kCh/8, (g+1) kCh/8), issued at 8 points of the tile
   auto issue_group = [&](int g) {
-    if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + 64 * (lane % B)];
+    if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + kSpan * (lane % kCh)];
 #pragma unroll
-    for (int q = g * (B / 8); q < (g + 1) * (B / 8); ++q)
-      pf[q] = buf_load<RawT>(rsrc, next_off + (uint32_t)((FLIP ? -64 : 64) * q * (int)sizeof(RawT)));
+    for (int q = g * (kCh / 8); q < (g + 1) * (kCh / 8); ++q)
+      pf[q] = buf_load<LoadT>(rsrc, next_off + (uint32_t)((FLIP ? -kSpan : kSpan) * q * (int)sizeof(RawT)));
   };
 
 #if XA_STAMPS
@@ -495,17 +541,34 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       };
       if (fast) {
         if (MIX) {
-          if (ln < B) cq[ln] = cqv;
+          if (ln < kCh) cq[ln] = cqv;
           __builtin_amdgcn_wave_barrier();
         }
+        if constexpr (XA_WIDE) {
+          // the 64 rows lie contiguous (both halves at once): sample s at row s/B, col s%B;
+          // chunk q's pair of lane l is row 4q + l/16, cols 2 (l%16) + {0, 1}: one b128
+          const LP4 st2 = (LP4)(buf + (ln / 16) * kRow + 2 * (ln % 16));
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
+          for (int q = 0; q < kCh; ++q) {
+            // FLIP: the pair was read from descending addresses, so its halves swap
+            v2f x0 = cvt_raw<DT>(FLIP ? pf[q].b : pf[q].a), x1 = cvt_raw<DT>(FLIP ? pf[q].a : pf[q].b);
+            if constexpr (MIX) {
+              const v2f c = cq[q];
+              x0 = cmul2(x0, cmul2(c, wl0));
+              x1 = cmul2(x1, cmul2(c, wl1));
+            }
+            st2[q * (4 * kRow / 2)] = v4f{x0.x, x0.y, x1.x, x1.y};
+          }
+        } else {
 #pragma unroll
-          for (int qq = 0; qq < B / 2; ++qq) {
-            const int q = hf * (B / 2) + qq;
-            v2f x = cvt_raw<DT>(pf[q]);
-            if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl));
-            st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = x;
+          for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+            for (int qq = 0; qq < B / 2; ++qq) {
+              const int q = hf * (B / 2) + qq;
+              v2f x = cvt_raw<DT>(pf[q]);
+              if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl0));
+              st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = x;
+            }
           }
         }
         read_all_rows();
@@ -521,9 +584,9 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     }
     next_fast = tau + 1 < nt && fast_tile(base + T);  // wave-uniform
     next_i0 = base + T - kPad;
-    {
-      const int i0 = base + T - kPad + ln;
-      next_off = (uint32_t)((FLIP ? in.len - 1 - i0 : (int64_t)i0) * (int64_t)sizeof(RawT));
+    {  // (FLIP: the pair's elements i0, i0 + 1 sit at len-1-i0 and len-2-i0)
+      const int i0 = base + T - kPad + kPer * ln;
+      next_off = (uint32_t)((FLIP ? in.len - kPer - i0 : (int64_t)i0) * (int64_t)sizeof(RawT));
     }
     // the next tile's loads: groups 0-3 now, 4-5 after the forward pass, 6-7 after the scan
     // (later issue points leave the register allocator room it does not use: spills; all
