@@ -47,9 +47,6 @@
 #ifndef XA_STAMPS
 #define XA_STAMPS 0
 #endif
-#ifndef XA_WIDE
-#define XA_WIDE 1  // tile loads and output stores two elements per lane (0: one)
-#endif
 
 namespace zfft {
 namespace xa {
@@ -70,9 +67,9 @@ struct Geo {
   static constexpr int kHeldRow = K + 2;     // output-transpose rows (v2f): b128 writes conflict-free
   static constexpr int kOutChunks = K;       // 64-output chunks per tile
   static constexpr int kRowsPerChunk = 64 / B > 0 ? 64 / B : 1;  // input rows one 64-sample chunk fills
-  // LDS per wave: half-tile transposes + FIR carry (12 used) + frame-end v carry (the 64 v
-  // before the last tile) + LO chunk starts (B)
-  static constexpr int kBuf = kHalves * kHalfRows * kRow + 16 + 64 + B;
+  // LDS per wave: the tile transpose (both halves) + FIR carry (12 used) + frame-end v
+  // carry (the 64 v before the last tile)
+  static constexpr int kBuf = kHalves * kHalfRows * kRow + 16 + 64;
   static constexpr int kWavesPerSimd = B == 32 ? 2 : 1;  // the register budget is cut for
 };
 
@@ -345,7 +342,6 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   LP buf = buf0;
   LP pcarry = buf + kHalves * kHalfRows * kRow;  // lane 63's FIR neighbour part, for next lane 0
   LP vcarry = pcarry + 16;                  // the 64 v before the last tile
-  LP cq = vcarry + 64;                      // lo at the B chunk starts of the tile
   const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
   const int nt = (e + 15) / T + 1;  // the last FIR/backward tile reaches e - 1
   v2f *__restrict__ o = out + (int64_t)f * n_out;
@@ -403,7 +399,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       v2f vc[kChunks];
       // wide: the final outputs 0 .. 128 nw - 1 as pairs (128 C + 2 ln + {0, 1}: row 8 C +
       // ln/8, cols 2 (ln%8) + {0, 1}; one b128 read, one 16-B store), the rest one per lane
-      constexpr int nw = XA_WIDE ? (kChunks - kLagChunks) / 2 : 0;
+      constexpr int nw = (kChunks - kLagChunks) / 2;
       v4f vw[nw > 0 ? nw : 1];
       if constexpr (nw > 0) {
         const LP4 hr2 = (LP4)(buf + (ln / 8) * kHeldRow + 2 * (ln % 8));
@@ -475,12 +471,13 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   typedef typename Raw<DT>::T RawT;
   const RawT *__restrict__ src = (const RawT *)in.p + (int64_t)f * in.stride;
   auto fast_tile = [&](int b) { return b >= kPad && b + T <= n + kPad; };
-  // narrow (XA_WIDE 0): chunk q = samples 64 q + lane; wide: chunk q = samples 128 q +
-  // 2 lane + {0, 1}, a pair per lane -- half the load (and LDS write) instructions
-  constexpr int kPer = XA_WIDE ? 2 : 1;  // elements per lane and chunk
-  constexpr int kCh = B / kPer;          // input chunks per tile
-  constexpr int kSpan = 64 * kPer;       // samples per chunk
-  typedef typename std::conditional<XA_WIDE, Pair<DT>, RawT>::type LoadT;
+  // chunk q = samples 128 q + 2 lane + {0, 1}: a pair per lane (16 B for complex64; one
+  // element per lane measured 4.5 % slower at stage 0)
+  constexpr int kPer = 2;           // elements per lane and chunk
+  constexpr int kCh = B / kPer;     // input chunks per tile
+  constexpr int kSpan = 64 * kPer;  // samples per chunk
+  static_assert(B == 32, "the pair layout of the tile loads assumes 32-sample lane rows");
+  typedef Pair<DT> LoadT;
   // lo[n0 + l] = lo[n0] lo[l] / sqrt(2): the chunk start times a per-lane factor (one per
   // element of the lane); lo has >= 2048 entries whenever a fast tile exists (L > 2048)
   v2f wl0 = splat(0.f), wl1 = splat(0.f);
@@ -518,7 +515,6 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       buf = b;
       pcarry = buf + kHalves * kHalfRows * kRow;
       vcarry = pcarry + 16;
-      cq = vcarry + 64;
     }
     const int base = tau * T;
     const bool last = tau == nt - 1;
@@ -540,12 +536,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
         __builtin_amdgcn_wave_barrier();
       };
       if (fast) {
-        if (MIX) {
-          if (ln < kCh) cq[ln] = cqv;
-          __builtin_amdgcn_wave_barrier();
-        }
-        if constexpr (XA_WIDE) {
-          // the 64 rows lie contiguous (both halves at once): sample s at row s/B, col s%B;
+        {  // the 64 rows lie contiguous (both halves at once): sample s at row s/B, col s%B;
           // chunk q's pair of lane l is row 4q + l/16, cols 2 (l%16) + {0, 1}: one b128
           const LP4 st2 = (LP4)(buf + (ln / 16) * kRow + 2 * (ln % 16));
 #pragma unroll
@@ -553,22 +544,11 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
             // FLIP: the pair was read from descending addresses, so its halves swap
             v2f x0 = cvt_raw<DT>(FLIP ? pf[q].b : pf[q].a), x1 = cvt_raw<DT>(FLIP ? pf[q].a : pf[q].b);
             if constexpr (MIX) {
-              const v2f c = cq[q];
+              const v2f c = lane_of(cqv, q);  // lane q holds chunk q's start (LDS: 1 % slower)
               x0 = cmul2(x0, cmul2(c, wl0));
               x1 = cmul2(x1, cmul2(c, wl1));
             }
             st2[q * (4 * kRow / 2)] = v4f{x0.x, x0.y, x1.x, x1.y};
-          }
-        } else {
-#pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-            for (int qq = 0; qq < B / 2; ++qq) {
-              const int q = hf * (B / 2) + qq;
-              v2f x = cvt_raw<DT>(pf[q]);
-              if constexpr (MIX) x = cmul2(x, cmul2(cq[q], wl0));
-              st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = x;
-            }
           }
         }
         read_all_rows();
