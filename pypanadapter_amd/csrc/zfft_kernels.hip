@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(InDesc in, int fra
   const int lrow = w.lane >> 4, lcol = w.lane & 15;
 
   auto xm = [&](int f, int i) -> v2f {  // mixed sample i of the window of frame f
-    return cmul(load_in_t<DT>(in, f, o + i), lob[i]);
+    return cmul2(load_in_t<DT>(in, f, o + i), lob[i]);
   };
   auto ext_slow = [&](int f, int j) -> v2f {
     if (f >= frames || j < 0 || j >= e) return splat(0.f);
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(InDesc in, int fra
     if (fast) {
       const v2f l = lob[j - kPad];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) pf[q] = cmul(load_in_t<DT>(in, f0 + lrow + 4 * q, o + j - kPad), l);
+      for (int q = 0; q < 16; ++q) pf[q] = cmul2(load_in_t<DT>(in, f0 + lrow + 4 * q, o + j - kPad), l);
     } else {
 #pragma unroll
       for (int q = 0; q < 16; ++q) pf[q] = ext_slow(f0 + 4 * q + lrow, j);
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(InDesc in, const v2f *__res
   if (k >= total) return;
   const int64_t f = k / in.len, i = k - f * in.len;
   const v2f v = load_in_t<DT>(in, f, i);
-  out[k] = lo ? cmul(v, lo[i]) : v;
+  out[k] = lo ? cmul2(v, lo[i]) : v;
 }
 
 // ------------------------------------------------------------------ Welch row
@@ -444,7 +444,20 @@ __device__ __forceinline__ int welch_slot(const WelchGeom &g, int k, float &mult
 }
 
 // ---- in-register DFTs (forward, exp(-2 pi i k n / R)) ----
-__device__ __forceinline__ v2f mul_negi(v2f a) { return v2f{a.y, -a.x}; }  // -i * a
+// Complex products here are cmul2 (two VOP3P instructions; the plain form compiles to four
+// and a nop) and the -i rotations fold into the operand selects of one add (add/sub_negi).
+// a + (-i) d = (a.x + d.y, a.y - d.x) and a - (-i) d = (a.x - d.y, a.y + d.x): one VOP3P add
+// each, the swap and sign in the operand selects (the plain form costs moves)
+__device__ __forceinline__ v2f add_negi(v2f a, v2f d) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(d));
+  return r;
+}
+__device__ __forceinline__ v2f sub_negi(v2f a, v2f d) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(d));
+  return r;
+}
 
 template <int R>
 __device__ __forceinline__ void dft(v2f *v);
@@ -458,11 +471,11 @@ __device__ __forceinline__ void dft<2>(v2f *v) {
 
 template <>
 __device__ __forceinline__ void dft<4>(v2f *v) {
-  const v2f a0 = v[0] + v[2], a1 = v[0] - v[2], a2 = v[1] + v[3], a3 = mul_negi(v[1] - v[3]);
+  const v2f a0 = v[0] + v[2], a1 = v[0] - v[2], a2 = v[1] + v[3], d = v[1] - v[3];
   v[0] = a0 + a2;
-  v[1] = a1 + a3;
+  v[1] = add_negi(a1, d);  // a1 + (-i) d
   v[2] = a0 - a2;
-  v[3] = a1 - a3;
+  v[3] = sub_negi(a1, d);
 }
 
 // W_16^m for m = 0..15 as compile-time constants
@@ -485,7 +498,7 @@ __device__ __forceinline__ void dft<8>(v2f *v) {
     dft<4>(a[n2]);
   }
 #pragma unroll
-  for (int k1 = 1; k1 < 4; ++k1) a[1][k1] = cmul(a[1][k1], w16(2 * k1));
+  for (int k1 = 1; k1 < 4; ++k1) a[1][k1] = cmul2(a[1][k1], w16(2 * k1));
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) {
     v[k1] = a[0][k1] + a[1][k1];
@@ -506,7 +519,7 @@ __device__ __forceinline__ void dft<16>(v2f *v) {
 #pragma unroll
   for (int n2 = 1; n2 < 4; ++n2)
 #pragma unroll
-    for (int k1 = 1; k1 < 4; ++k1) a[n2][k1] = cmul(a[n2][k1], w16(n2 * k1));
+    for (int k1 = 1; k1 < 4; ++k1) a[n2][k1] = cmul2(a[n2][k1], w16(n2 * k1));
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) {
     v2f b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
@@ -519,23 +532,23 @@ __device__ __forceinline__ void dft<16>(v2f *v) {
 // v[r] *= b^r, r = 1..15, from bp = {b, b^2, b^4, b^8}: each power applied as soon as it
 // is formed (at most eight of them live)
 __device__ __forceinline__ void apply_powers(v2f *v, const v2f *bp) {
-  v[1] = cmul(v[1], bp[0]);
-  v[2] = cmul(v[2], bp[1]);
-  v[4] = cmul(v[4], bp[2]);
-  v[8] = cmul(v[8], bp[3]);
-  const v2f w3 = cmul(bp[0], bp[1]), w5 = cmul(bp[0], bp[2]), w6 = cmul(bp[1], bp[2]);
-  const v2f w7 = cmul(w3, bp[2]);
-  v[3] = cmul(v[3], w3);
-  v[5] = cmul(v[5], w5);
-  v[6] = cmul(v[6], w6);
-  v[7] = cmul(v[7], w7);
-  v[9] = cmul(v[9], cmul(bp[0], bp[3]));
-  v[10] = cmul(v[10], cmul(bp[1], bp[3]));
-  v[11] = cmul(v[11], cmul(w3, bp[3]));
-  v[12] = cmul(v[12], cmul(bp[2], bp[3]));
-  v[13] = cmul(v[13], cmul(w5, bp[3]));
-  v[14] = cmul(v[14], cmul(w6, bp[3]));
-  v[15] = cmul(v[15], cmul(w7, bp[3]));
+  v[1] = cmul2(v[1], bp[0]);
+  v[2] = cmul2(v[2], bp[1]);
+  v[4] = cmul2(v[4], bp[2]);
+  v[8] = cmul2(v[8], bp[3]);
+  const v2f w3 = cmul2(bp[0], bp[1]), w5 = cmul2(bp[0], bp[2]), w6 = cmul2(bp[1], bp[2]);
+  const v2f w7 = cmul2(w3, bp[2]);
+  v[3] = cmul2(v[3], w3);
+  v[5] = cmul2(v[5], w5);
+  v[6] = cmul2(v[6], w6);
+  v[7] = cmul2(v[7], w7);
+  v[9] = cmul2(v[9], cmul2(bp[0], bp[3]));
+  v[10] = cmul2(v[10], cmul2(bp[1], bp[3]));
+  v[11] = cmul2(v[11], cmul2(w3, bp[3]));
+  v[12] = cmul2(v[12], cmul2(bp[2], bp[3]));
+  v[13] = cmul2(v[13], cmul2(w5, bp[3]));
+  v[14] = cmul2(v[14], cmul2(w6, bp[3]));
+  v[15] = cmul2(v[15], cmul2(w7, bp[3]));
 }
 
 // LDS index with one pad slot per 16 (breaks the power-of-two strides of the passes)
@@ -562,7 +575,7 @@ __device__ __forceinline__ void stockham_pass(v2f *v, int t, int N, int Ns,
         apply_powers(w, bp);
       } else {
 #pragma unroll
-        for (int r = 1; r < R; ++r) w[r] = cmul(w[r], tw[r * ts]);
+        for (int r = 1; r < R; ++r) w[r] = cmul2(w[r], tw[r * ts]);
       }
     }
     dft<R>(w);
@@ -898,7 +911,7 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
 #pragma unroll
         for (int m = 0; m < RL; ++m) {
           a0 += blkv[m];
-          a1 += m == 0 ? blkv[0] : cmul(blkv[m], w16((16 - (16 / RL) * m) & 15));
+          a1 += m == 0 ? blkv[0] : cmul2(blkv[m], w16((16 - (16 / RL) * m) & 15));
         }
         acc[2 * u] = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, acc[2 * u]));
         acc[2 * u + 1] = fmaf(a1.x, a1.x, fmaf(a1.y, a1.y, acc[2 * u + 1]));
@@ -1009,11 +1022,11 @@ __global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict_
     const v2f a = tw[n1 * t];
     v2f bp[4];
     bp[0] = tw[16 * n1];
-    bp[1] = cmul(bp[0], bp[0]);
-    bp[2] = cmul(bp[1], bp[1]);
-    bp[3] = cmul(bp[2], bp[2]);
+    bp[1] = cmul2(bp[0], bp[0]);
+    bp[2] = cmul2(bp[1], bp[1]);
+    bp[3] = cmul2(bp[2], bp[2]);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = cmul(v[i], a);
+    for (int i = 0; i < 16; ++i) v[i] = cmul2(v[i], a);
     apply_powers(v, bp);
   }
   v2f *__restrict__ zs = z + (int64_t)fs * N;
