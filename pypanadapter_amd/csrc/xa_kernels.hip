@@ -11,21 +11,24 @@
 //   g = h / D2(1/w)                        backward all-pole cascade, output rate
 //
 // so a stage costs 8 + 12.5 + 4 packed multiply-adds per input sample, against 2 x 17 for
-// two DF2T passes.  A wave walks its frame in tiles of 64 lanes x B samples (B = 32 or 64;
-// lane i owns the sub-block of B consecutive samples, K = B/2 kept outputs):
-//  forward:   every lane runs the all-pole cascade from a zero state over its B samples;
-//             its end state goes to the real modal basis (T^-1, block lower triangular,
-//             one rotation-scaling 2x2 block per pole pair), a Kogge-Stone scan over
-//             lanes -- per mode only as deep as its radius needs (xa_levels) -- gives each
-//             lane its entering state, and pass 2 reruns the cascade from it.  The tile's
-//             entering state is folded into lane 0.
+// two DF2T passes.  A wave walks its frame in tiles of 64 lanes x B = 32 samples (lane i
+// owns the sub-block of B consecutive samples, K = B/2 kept outputs), loaded a tile ahead
+// as pairs of consecutive samples per lane and transposed to lane rows through LDS:
+//  forward:   every lane runs the all-pole cascade once, from a zero state, over its B
+//             samples, streaming v into the FIR; its end state goes to the real modal
+//             basis (T^-1, block lower triangular, one rotation-scaling 2x2 block per pole
+//             pair), a Kogge-Stone scan over lanes -- per mode only as deep as its radius
+//             needs (xa_levels) -- gives each lane its exact entering state, whose
+//             zero-input response through the FIR is added from precomputed tables (gown,
+//             gnb) instead of a second pass.  The tile's entering state is folded into lane 0.
 //  FIR:       lane i evaluates h at the K odd positions of [B i - 16, B i + B - 16) from
 //             v[B i - 24, B i + B): its own v and the last 24 v of lane i-1, whose share
 //             lane i-1 accumulates itself and hands over with one DPP shift (lane 0 takes
 //             the previous tile's lane-63 share from LDS).
-//  backward:  the same scheme on the K h values of each lane, descending, with the
-//             state entering the tile from above provisionally zero; the state it leaves
-//             at the tile bottom is exact regardless (its dependence on the top state is
+//  backward:  one pass on the K h values of each lane, descending, from a zero state, the
+//             scan down, and the entering state's response from the lag rows; the state
+//             entering the tile from above is provisionally zero, the state it leaves at
+//             the tile bottom is exact regardless (its dependence on the top state is
 //             |lambda^2|^(32 B) < 1e-29) and is the top state of the tile below, processed
 //             one step earlier: that tile's top kXaLag outputs get C A2^d T q, then all
 //             its outputs are stored.
@@ -40,7 +43,6 @@
 // Numerics: float32, max relative error ~8e-6 of the decimated IQ vs float64 sosfiltfilt
 // (plain float32 sosfiltfilt: ~1e-6); end-to-end rows within 1e-5 dB (tools/xa_proto.py).
 #include <cstddef>
-#include <type_traits>
 
 #include "zfft_device.h"
 
