@@ -572,9 +572,16 @@ bool auto_xa(int frames, int64_t L) {
   return frames >= kXaMinFrames || (frames >= kXaMinFramesShort && L <= kXaShortFrame);
 }
 
-bool use_fused(const zfft_plan *p, int64_t L) {
+// The fused blocked schedule (path 2) saves passes over the frame interior but adds the
+// exact edge-window runs, whose launches cost about as much as a whole pass over a few
+// frames: it wins only for large batches.  Measured on MI355X (frames x samples, ms, path 1
+// / path 2): cfg2 1 x 299008 0.46 / 0.94, 64 x 0.51 / 0.95, 256 x 1.19 / 1.52; cfg1 256 x
+// 262144 1.30 / 1.32; cfg5 64 x 1048576 1.11 / 1.41, 256 x 4.12 / 3.68.
+constexpr int64_t kFusedMinSamples = (int64_t)1 << 28;  // per call
+bool use_fused(const zfft_plan *p, int64_t L, int frames) {
   if (p->path == 1 || p->K < 2) return false;
-  return 8 * edge_window(p->K) <= L;  // windows cost <= 1/4 of a frame
+  if (8 * edge_window(p->K) > L) return false;  // windows cost <= 1/4 of a frame
+  return p->path == 2 || (int64_t)frames * L >= kFusedMinSamples;
 }
 
 int fused_block(int64_t n_mid, int ngroups) {
@@ -695,7 +702,7 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   // blocked schedules split each frame over many waves and win for a few frames per call
   if (p->path == 3 || (p->path == 0 && auto_xa(frames, L)))
     return run_xa(p, in, frames, n, out, st);
-  if (use_fused(p, L)) return run_fused(p, in, L, frames, n, out, st);
+  if (use_fused(p, L, frames)) return run_fused(p, in, L, frames, n, out, st);
   return run_exact(p, in, p->lo.as<float2>(), frames, n, out, st);
 }
 

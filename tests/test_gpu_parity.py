@@ -338,3 +338,29 @@ def test_facade_matches_reference_rows():
     assert_row_close(row, golden_rows()["cfg2"], "psd_row")
     assert_row_close(thread_psd_row(x, 2.4e6, 4096, 8), golden_rows()["T_cfg2"], "thread")
     assert thread_psd_row(x[:4000], 2.4e6, 4096, 8) is None  # T:1522-1523
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F,L,want", [(1, 299008, "exact"), (64, 1048576, "exact"),
+                                      (256, 1048576, "fused"), (1024, 299008, "xa")])
+def test_auto_schedule_by_batch(F, L, want):
+    """The automatic decimator schedule follows the measured crossovers (zfft_plan.cpp
+    auto_xa / use_fused): one frame per call -- the reference's use -- and small batches run
+    the exact blocked passes, only batches of >= 2^28 samples the fused interior with edge
+    windows, and >= 1024 frames the XA tiles."""
+    import torch
+    from pypanadapter_amd import ZoomFFT
+    dev = torch.device("cuda", 0)
+    x = torch.zeros((F, L, 2), dtype=torch.float32, device=dev)
+    x[..., 0] = 1.0
+    rows = torch.empty((F, 512), dtype=torch.float32, device=dev)
+    with ZoomFFT(4096, 8, 2.4e6, n_win=512) as plan:
+        plan.set_timing(True)
+        plan.process_device(x.data_ptr(), L, F, rows.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        names = plan.launch_names()
+    first = {"exact": "exact_forward_mix", "fused": "exact_forward_mix", "xa": "xa_stage_mix"}[want]
+    assert names[0] == first, names
+    assert ("edge_windows" in names) == (want == "fused"), names
+    del x, rows
+    torch.cuda.empty_cache()
