@@ -113,9 +113,10 @@ class ZoomFFT:
         return [n for n in raw.decode().split(",") if n]
 
     def set_path(self, path: int) -> None:
-        """0 auto, 1 exact reference pass order (blocked), 2 fused interior + exact edges
-        (blocked), 3 XA tiles (all-pole + FIR + half-rate all-pole, one wave per frame; the
-        auto choice for >= 1024 frames, or >= 512 frames of <= 2^19 samples)."""
+        """0 auto, 1 exact reference pass order (blocked; the auto choice for small batches,
+        e.g. one frame per call), 2 fused interior + exact edges (blocked; auto from 2^28
+        samples per call), 3 XA tiles (all-pole + FIR + half-rate all-pole, one wave per
+        frame; auto for >= 1024 frames, or >= 512 frames of <= 2^19 samples)."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
 
     def set_welch(self, mode: int) -> None:
