@@ -364,3 +364,32 @@ def test_auto_schedule_by_batch(F, L, want):
     assert ("edge_windows" in names) == (want == "fused"), names
     del x, rows
     torch.cuda.empty_cache()
+
+
+# frame lengths around the XA tile geometry (T = 2048 input samples per tile, odd
+# extension 27 each side): no fast tile, exactly one, a fast tile ending at n + 27, the
+# last tile reaching e - 1 exactly, odd and power-of-two lengths
+XA_EDGE_LENGTHS = [28, 100, 2048 + 26, 2048 + 27, 2048 + 28, 4096 + 53, 4096 + 54, 4096 + 55,
+                   6144 - 27, 8192, 8192 + 1, 10007, 3 * 2048 + 2048 // 2, 32769]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("z", [2, 8])
+@pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
+def test_xa_decimate_tile_boundary_lengths(oracle_lib, z, flip):
+    """XA (path 3) decimated IQ at frame lengths around its tile boundaries, every stage,
+    against the float64 oracle (relative to the output peak, XA's documented tolerance);
+    flip reverses the frame on load as the sources do (S:541-543)."""
+    from pypanadapter_amd import ZoomFFT
+    rng = np.random.default_rng(90 + z)
+    for L in XA_EDGE_LENGTHS:
+        if (L + z - 1) // z < 28:  # the last stage would be <= padlen: the reference raises
+            continue
+        x = (rng.standard_normal(L) + 1j * rng.standard_normal(L)).astype(np.complex64)
+        with ZoomFFT(32, z, 2.4e6, flip=flip) as plan:
+            plan.set_path(3)
+            d = plan.decimate(x)
+        ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, z, 2.4e6)
+        assert d.shape == ref.shape, (L, d.shape, ref.shape)
+        err = np.abs(d - ref).max() / np.abs(ref).max()
+        assert err < 1e-5 * np.log2(z), (L, z, flip, float(err))
