@@ -438,9 +438,12 @@ std::vector<int64_t> stage_lengths(int64_t L, int K) {
 int choose_block(const zfft_plan *p, int64_t n, int ngroups) {
   if (p->block_override > 0) return (p->block_override + 15) & ~15;
   // Enough waves (one per block of a 64-frame group) to fill 256 CUs many times over;
-  // larger blocks amortise the warm-up.
+  // larger blocks amortise the warm-up.  A few frames of <= 2^19 samples (one per call:
+  // the reference's use) go down to 256-sample blocks, whose shorter serial runs took one
+  // cfg2 frame from 0.48 to 0.38 ms of kernels (cfg5's 2^20-sample frames: no gain).
+  const int s_min = n <= ((int64_t)1 << 19) ? 256 : 512;
   int S = 4096;
-  while (S > 512 && (int64_t)ngroups * ((n + kPad + S - 1) / S) < 8192) S >>= 1;
+  while (S > s_min && (int64_t)ngroups * ((n + kPad + S - 1) / S) < 8192) S >>= 1;
   return S;
 }
 
