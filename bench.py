@@ -150,6 +150,23 @@ def parity_check(frames: dict, rows: dict, cfg, f_lo: float) -> dict:
             "pass": bool(worst_db <= 1e-3 and worst_amp <= 1e-5)}
 
 
+def provenance() -> dict:
+    """Ties this line to the profiles/ it is judged against: the kernel-source hash (the
+    stamp PMC/SQ summaries carry), the git commit the library was built at (the GPU box has
+    no .git: build() records it next to the .so), and whether that build matches the tree."""
+    from pypanadapter_amd import build
+    info = build.build_info()
+    head = None
+    try:
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or None
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return {"source_hash": build.source_hash(), "git_head": head or info.get("git_head"),
+            "git_head_from": "git" if head else "build_info", "built_source_hash": info.get("source_hash"),
+            "built_git_dirty": info.get("git_dirty"), "host": socket.gethostname()}
+
+
 # ----------------------------------------------------------------------------- launcher
 def spawn_ranks(argv) -> int:
     """`--gpus N` outside torch.distributed.run: N rank processes, one per GPU, started
@@ -291,7 +308,10 @@ def end_to_end(torch, args, cfg, x_dev, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200, help="timed steps (default: >= 1 s at cfg2)")
+    ap.add_argument("--steps", type=int, default=200,
+                    help="timed steps; raised so that the timed region lasts >= --min-seconds")
+    ap.add_argument("--min-seconds", type=float, default=1.0,
+                    help="lower bound on the timed region (0: exactly --steps)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per rank (default: config)")
@@ -377,17 +397,25 @@ def main():
         plan.process_device(xe.data_ptr(), L, F, rows.data_ptr(), sp)
         plan.waterfall_push_device(rows.data_ptr(), F, sp)
 
-    for _ in range(args.warmup):
+    t_w = time.perf_counter()
+    for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize(dev)
+    est = (time.perf_counter() - t_w) / max(1, args.warmup)
+    # >= min_seconds of timed work whatever --steps says (a 20-step region at ~6 ms/step is
+    # 0.13 s, inside the box-to-box noise); every rank runs the same count (max over ranks)
+    steps = max(args.steps, math.ceil(args.min_seconds / max(est, 1e-6)))
     if dist:
+        ts = torch.tensor([steps], dtype=torch.int64)
+        dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+        steps = int(ts[0])
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
@@ -402,7 +430,7 @@ def main():
 
     # per-launch HIP-event times (events on the launch stream) over a few instrumented steps
     plan.set_timing(True)
-    acc, n_inst = {}, max(1, min(args.steps, 10))
+    acc, n_inst = {}, max(1, min(steps, 10))
     for _ in range(n_inst):
         plan.process_device(xe.data_ptr(), L, F, rows.data_ptr(), sp)
         for i, (nm, ms) in enumerate(zip(plan.launch_names(), plan.timings())):
@@ -428,13 +456,13 @@ def main():
         del rows
         e2e = end_to_end(torch, args, cfg, x if x is not None else xe, dev)
 
-    ms_per_step = wall_max / args.steps * 1e3
-    total_samples = F * L * args.steps * world
+    ms_per_step = wall_max / steps * 1e3
+    total_samples = F * L * steps * world
     value = total_samples / wall_max / 1e6
-    lines = F * args.steps * world / wall_max
+    lines = F * steps * world / wall_max
     bps = IN_BYTES[args.in_dtype]
     alg_step = F * alg_bytes_per_line(bps, L, W)
-    ev_ms_step = ev_max / args.steps * 1e3
+    ev_ms_step = ev_max / steps * 1e3
     path_gbs = alg_step / (ev_ms_step / 1e3) / 1e9
     dominant = max(kernels, key=lambda k: kernels[k]) if kernels else None
     traffic_j, traffic_status = stamped_profile(
@@ -459,8 +487,10 @@ def main():
         "value": round(value, 2),
         "unit": "MS/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": steps,
+        "steps_requested": args.steps,
         "warmup": args.warmup,
+        "timed_seconds": round(wall_max, 4),
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -490,6 +520,7 @@ def main():
         "parity_checked_frames": check,
         "end_to_end": e2e,
         "cpu_baseline": cpu,
+        "provenance": provenance(),
     }
     print(json.dumps(out))
     if dist:

@@ -119,7 +119,11 @@ int64_t zfft_decimated_length(int64_t n_samples, int32_t zoom);
 
 /* Waterfall ring: H = n_win/4 rows of n_win floats, reference row order on read. */
 int zfft_waterfall_push(zfft_plan *plan, const float *row /* host, n_win; NULL = last row of
-                                                             the last zfft_process* frame */);
+                                                             the last zfft_process* frame:
+                                                             ZFFT_EINVAL when the plan's rows
+                                                             are shorter than n_win */);
+/* d_rows: count rows of n_win floats, every column defined (a row shorter than n_win --
+ * zfft_plan_row_length < n_win -- leaves its tail columns unwritten: pad them first). */
 int zfft_waterfall_push_device(zfft_plan *plan, const float *d_rows, int32_t count,
                                void *hip_stream);
 int zfft_waterfall_read(zfft_plan *plan, float *img_out /* host, H*n_win */);
@@ -178,24 +182,31 @@ int zfft_plan_tune(zfft_plan *plan, int32_t block, int32_t warmup);
 
 /* Per-launch HIP-event timing of zfft_process*: when enabled, the plan brackets every
  * kernel it launches with events on the launch stream; zfft_plan_timings then returns the
- * durations (ms) of the last call, in launch order: for each decimation stage k the
- * forward and backward pass, then the Welch-row kernel.  Diagnostics; adds event records. */
+ * durations (ms) of the last call, in launch order, named by zfft_plan_timing_names: per
+ * decimation stage one "xa_stage_mix"/"xa_stage" interval (XA schedule) or a forward and a
+ * backward pass (blocked schedules), then the Welch kernel ("welch_rows" / "welch4").  A
+ * batched zfft_process call reports every batch ("batch_wait" = the gap before batch k >= 1,
+ * mostly its H2D copy).  Diagnostics; adds event records. */
 int zfft_plan_timing(zfft_plan *plan, int32_t enable);
 int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *count);
 /* Comma-separated names of the intervals zfft_plan_timings returns (owned by the plan). */
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
 /* Decimator schedule: 0 = automatic (3 for batches of >= 1024 frames, or >= 512 frames of
- * <= 2^19 samples; otherwise 2 for batches of >= 2^28 samples whose frames are long enough
- * for the edge windows, else 1 -- e.g. one frame per call, the reference's use),
+ * <= 2^19 samples -- a batched zfft_process call is judged by its whole frame count;
+ * otherwise 2 for batches of >= 2^28 samples whose frames are long enough for the edge
+ * windows, else 1 -- e.g. one frame per call, the reference's use),
  * 1 = blocked warm-up passes in the reference order (frames split over many waves),
  * 2 = blocked, fused commuted-order interior + exact edge windows, 3 = XA tiles (one wave per
- * frame: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned, no
- * intermediate in memory).  All produce the reference's rows within the fp32 parity gate;
- * diagnostics / A-B only (zfft_plan.cpp auto_xa, use_fused). */
+ * frame and stage: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned;
+ * each stage is one launch whose decimated output -- n_k/2 complex64 per frame -- is the next
+ * stage's input in device memory).  Path 3 needs every stage array below 2^31 bytes per frame
+ * (ZFFT_EUNSUPPORTED when forced beyond; auto picks a blocked path there).  All produce the
+ * reference's rows within the fp32 parity gate; diagnostics / A-B only (zfft_plan.cpp
+ * auto_xa, use_fused). */
 int zfft_plan_path(zfft_plan *plan, int32_t path);
 
-/* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 16384, four-step
+/* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 8192, four-step
  * beyond), 1 = one workgroup per frame (n_fft <= 16384), 2 = four-step N1 x 256 (n_fft in
  * [4096, 65536]).  Same rows within the parity gate; diagnostics / A-B only. */
 int zfft_plan_welch(zfft_plan *plan, int32_t mode);

@@ -42,7 +42,40 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH,
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
+    if out == LIB_PATH and not defines:
+        _write_build_info()
     return out
+
+
+INFO_PATH = os.path.join(LIB_DIR, "build_info.json")
+
+
+def _git(*args):
+    try:
+        r = subprocess.run(["git", "-C", ROOT, *args], capture_output=True, text=True, timeout=10)
+        return r.stdout.strip() if r.returncode == 0 else None
+    except (OSError, subprocess.SubprocessError):
+        return None
+
+
+def _write_build_info() -> None:
+    """Next to the shipped .so (it travels with it; the GPU box has no .git): the source hash
+    and git commit it was built from, so a bench line can name both."""
+    import json
+    st = _git("status", "--porcelain", "--untracked-files=no")
+    info = {"source_hash": source_hash(), "git_head": _git("rev-parse", "HEAD"),
+            "git_dirty": None if st is None else bool(st), "arch": ARCH}
+    with open(INFO_PATH, "w") as fh:
+        json.dump(info, fh)
+
+
+def build_info() -> dict:
+    import json
+    try:
+        with open(INFO_PATH) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
 
 
 def source_hash() -> str:

@@ -392,6 +392,7 @@ struct zfft_plan {
   std::vector<std::string> mark_names;
   std::string names_buf;
   int n_marks = 0;
+  int sched_frames = 0;  // > 0 inside a batched zfft_process: the whole call's frame count
   int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows,
                 // 3 XA tiles (all-pole + FIR + half-rate all-pole)
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
@@ -427,6 +428,13 @@ void mark(zfft_plan *p, hipStream_t st, const char *what = "") {
   p->mark_names[p->n_marks] = what;
   (void)hipEventRecord(p->events[p->n_marks++], st);
 }
+
+// Scope of a batched zfft_process call: its batches are scheduled as the whole call.
+struct SchedFrames {
+  zfft_plan *p;
+  SchedFrames(zfft_plan *pl, int frames) : p(pl) { p->sched_frames = frames; }
+  ~SchedFrames() { p->sched_frames = 0; }
+};
 
 // Stage lengths: n_0 = L, n_{k+1} = ceil(n_k / 2)  (decimate(...)[::2]).
 std::vector<int64_t> stage_lengths(int64_t L, int K) {
@@ -575,6 +583,12 @@ bool auto_xa(int frames, int64_t L) {
   return frames >= kXaMinFrames || (frames >= kXaMinFramesShort && L <= kXaShortFrame);
 }
 
+// XA addresses a frame's stage input and output through 32-bit buffer resources.
+bool xa_fits(const zfft_plan *p, int64_t L) {
+  return L * (int64_t)in_elem_bytes(p->cfg.in_dtype) < ((int64_t)1 << 31) &&
+         L * (int64_t)sizeof(float2) < ((int64_t)1 << 31);
+}
+
 // The fused blocked schedule (path 2) saves passes over the frame interior but adds the
 // exact edge-window runs, whose launches cost about as much as a whole pass over a few
 // frames: it wins only for large batches.  Measured on MI355X (frames x samples, ms, path 1
@@ -699,13 +713,17 @@ int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t
 
 int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
                   const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
+  if (p->path == 3 && !xa_fits(p, L))
+    return fail(ZFFT_EUNSUPPORTED, "XA tiles (path 3) address a frame's stage arrays with 32-bit "
+                                   "offsets: frames of >= 2^31 bytes need path 0, 1 or 2");
   int rc = ensure_lo(p, L);
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  if (p->path == 3 || (p->path == 0 && auto_xa(frames, L)))
+  const int sf = std::max(frames, p->sched_frames);
+  if (p->path == 3 || (p->path == 0 && auto_xa(sf, L) && xa_fits(p, L)))
     return run_xa(p, in, frames, n, out, st);
-  if (use_fused(p, L, frames)) return run_fused(p, in, L, frames, n, out, st);
+  if (use_fused(p, L, sf)) return run_fused(p, in, L, frames, n, out, st);
   return run_exact(p, in, p->lo.as<float2>(), frames, n, out, st);
 }
 
@@ -737,8 +755,7 @@ int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, fl
   if (rc) return rc;
   const InDesc in = input_of(p, d_iq, L);
   const float2 *x = (const float2 *)d_iq;
-  p->n_marks = 0;
-  mark(p, st, "start");
+  if (p->n_marks == 0) mark(p, st, "start");  // (the entry points reset the marks per call)
   if (p->K > 0) {
     rc = run_decimator(p, in, L, frames, n, &x, st);
     if (rc) return rc;
@@ -1043,6 +1060,7 @@ int zfft_process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frame
   hipStream_t st = pick_stream(p, hip_stream);
   rc = use_stream(p, st);
   if (rc) return rc;
+  p->n_marks = 0;
   rc = process_device(p, d_iq, L, frames, d_rows, st);
   if (rc) return rc;
   return done_on(p, st);
@@ -1058,8 +1076,9 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
   // Batches: one for a small call; otherwise >= 2 so that the H2D copy of batch k+1 (copy
   // stream) runs while batch k is computed (plan stream).  From pinned memory both are
   // asynchronous; from pageable memory HIP stages the copy on this thread, which then copies
-  // batch k+1 while the GPU computes batch k.  Batches keep >= kXaMinFrames frames when the
-  // call has twice that, so the schedule is the one a device call of that size gets.
+  // batch k+1 while the GPU computes batch k.  The decimator schedule of every batch is the
+  // one the whole call would get (SchedFrames), so formats and batchings compare like for
+  // like; batches keep >= kXaMinFrames frames when the call has twice that (fuller waves).
   int B = frames;
   const size_t total = (size_t)frames * frame_bytes;
   if (total >= kPipeMinBytes && frames >= 2) {
@@ -1076,6 +1095,9 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
   if (rc == ZFFT_OK && nb > 1) rc = use_stream(p, p->copy_st);
   if (rc) return rc;
   const char *src = (const char *)iq;
+  p->n_marks = 0;  // timings cover every batch of this call
+  mark(p, p->stream, "start");
+  SchedFrames sched(p, frames);  // each batch gets the schedule of the whole call
   for (int k = 0; k < nb; ++k) {
     const int f0 = k * B, nk = std::min(B, frames - f0), buf = k & 1;
     void *dst = buf ? p->in2.p : p->in.p;
@@ -1086,6 +1108,7 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
     if (e == hipSuccess && nb > 1) e = hipEventRecord(p->h2d_ev[buf], cs);
     if (e == hipSuccess && nb > 1) e = hipStreamWaitEvent(p->stream, p->h2d_ev[buf], 0);
     if (e != hipSuccess) return hip_fail(e, "H2D copy");
+    if (k > 0) mark(p, p->stream, "batch_wait");
     rc = process_device(p, dst, L, nk, p->rows.as<float>() + (int64_t)f0 * p->cfg.n_win, p->stream);
     if (rc) return rc;
     if (nb > 1 && (e = hipEventRecord(p->comp_ev[buf], p->stream)) != hipSuccess)
@@ -1186,6 +1209,10 @@ int zfft_waterfall_push(zfft_plan *p, const float *row) {
     src = p->one_row.as<float>();
   }
   if (!src) return fail(ZFFT_EINVAL, "no row given and no frame processed yet");
+  if (!row && row_length(p) < p->W)  // columns >= row_length were never written
+    return fail(ZFFT_EINVAL, "the plan's rows are shorter than n_win (odd n_win, or the one-sided "
+                             "real-input crop): img_array[-1:] = psd raises in the reference "
+                             "(S:1640); push a full-width row instead");
   rc = zfft_waterfall_push_device(p, src, 1, p->stream);
   if (rc) return rc;
   hipError_t e = hipStreamSynchronize(p->stream);

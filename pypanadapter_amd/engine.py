@@ -100,11 +100,13 @@ class ZoomFFT:
         check(self.lib.zfft_plan_timing(self._plan, int(bool(enable))), "zfft_plan_timing")
 
     def timings(self) -> list:
-        """Per-launch ms of the last process call (needs set_timing(True)); launch order:
-        [fwd_0, bwd_0, fwd_1, bwd_1, ..., welch]."""
-        buf = (ctypes.c_float * 64)()
+        """Per-launch ms of the last process call (needs set_timing(True)), in launch order,
+        one per name of `launch_names()`: XA schedule [xa_stage_mix, xa_stage, ..., welch_rows
+        | welch4]; blocked schedules a forward and a backward pass per stage; a batched host
+        call repeats the sequence per batch after a "batch_wait" interval."""
+        buf = (ctypes.c_float * 1024)()
         n = ctypes.c_int32()
-        check(self.lib.zfft_plan_timings(self._plan, buf, 64, ctypes.byref(n)), "zfft_plan_timings")
+        check(self.lib.zfft_plan_timings(self._plan, buf, 1024, ctypes.byref(n)), "zfft_plan_timings")
         return [float(buf[i]) for i in range(n.value)]
 
     def launch_names(self) -> list:

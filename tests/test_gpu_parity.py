@@ -393,3 +393,48 @@ def test_xa_decimate_tile_boundary_lengths(oracle_lib, z, flip):
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
         err = np.abs(d - ref).max() / np.abs(ref).max()
         assert err < 1e-5 * np.log2(z), (L, z, flip, float(err))
+
+
+def test_plan_fed_push_refuses_short_rows():
+    """Odd W: the plan's rows hold W - 1 entries (the reference's slice), so pushing the
+    plan's own last row into a W-wide waterfall is refused -- the reference's
+    img_array[-1:] = psd raises there (S:1640) -- while a full-width host row still goes."""
+    from pypanadapter_amd import ZoomFFT
+    x = _frames(1, 65536, 1024, 8, 127, seed0=77)[0]
+    with ZoomFFT(1024, 8, 2.4e6, n_win=127) as plan:
+        assert plan.row_length == 126
+        plan.rows(x)
+        with pytest.raises(ValueError):
+            plan.waterfall_push()
+        plan.waterfall_push(np.full(127, -150.0, np.float32))
+        assert (plan.waterfall_image() == -150.0).all(axis=1).any()
+
+
+def test_xa_refuses_frames_beyond_32bit_offsets():
+    """Path 3 addresses a frame's stage arrays with 32-bit buffer offsets: forced on a frame
+    of >= 2^31 bytes it refuses before any launch (auto takes a blocked path there)."""
+    import torch
+    from pypanadapter_amd import ZoomFFT
+    d = torch.zeros(64, dtype=torch.float32, device="cuda")
+    rows = torch.empty(512, dtype=torch.float32, device="cuda")
+    with ZoomFFT(4096, 8, 2.4e6, n_win=512) as plan:
+        plan.set_path(3)
+        with pytest.raises(NotImplementedError):
+            plan.process_device(d.data_ptr(), 1 << 28, 1, rows.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream)
+
+
+def test_batched_host_call_times_every_batch_with_one_schedule():
+    """zfft_process splits a >= 64 MB call into batches (H2D of k+1 under compute of k):
+    the timings cover every batch, and every batch runs the schedule of the whole call."""
+    from pypanadapter_amd import ZoomFFT
+    F, L = 1024, 32768
+    x = np.zeros((F, L), np.complex64)
+    x[:, ::3] = 1.0
+    with ZoomFFT(1024, 8, 2.4e6) as plan:
+        plan.set_timing(True)
+        rows = plan.rows(x)
+        names = plan.launch_names()
+    assert np.all(np.isfinite(rows))
+    assert names.count("batch_wait") >= 1, names
+    assert names.count("xa_stage_mix") == names.count("batch_wait") + 1, names

@@ -39,6 +39,8 @@ for s in $STEPS; do
       run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
       run bench 900 python bench.py || exit $? ;;
+    driver)  # the driver's own bench command line
+      run bench_driver 900 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     quick)
       run quick 300 python bench.py --steps 100 --warmup 3 $FAST || exit $? ;;
     cfgs)
