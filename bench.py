@@ -397,14 +397,17 @@ def main():
         plan.process_device(xe.data_ptr(), L, F, rows.data_ptr(), sp)
         plan.waterfall_push_device(rows.data_ptr(), F, sp)
 
-    t_w = time.perf_counter()
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize(dev)
-    est = (time.perf_counter() - t_w) / max(1, args.warmup)
+    t_w = time.perf_counter()  # a warm probe for the step time (the first warmup step also
+    for _ in range(3):         # allocates the plan's workspaces)
+        step()
+    torch.cuda.synchronize(dev)
+    est = (time.perf_counter() - t_w) / 3
     # >= min_seconds of timed work whatever --steps says (a 20-step region at ~6 ms/step is
     # 0.13 s, inside the box-to-box noise); every rank runs the same count (max over ranks)
-    steps = max(args.steps, math.ceil(args.min_seconds / max(est, 1e-6)))
+    steps = max(args.steps, math.ceil(1.05 * args.min_seconds / max(est, 1e-6)))
     if dist:
         ts = torch.tensor([steps], dtype=torch.int64)
         dist.all_reduce(ts, op=dist.ReduceOp.MAX)

@@ -21,7 +21,14 @@ def _newest_input_mtime() -> float:
 
 
 def needs_build() -> bool:
-    return not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < _newest_input_mtime()
+    """The shipped .so is missing or was built from other sources (the hash build() records
+    next to it; file times when there is no record)."""
+    if not os.path.exists(LIB_PATH):
+        return True
+    info = build_info()
+    if info.get("source_hash"):
+        return info["source_hash"] != source_hash()
+    return os.path.getmtime(LIB_PATH) < _newest_input_mtime()
 
 
 def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH,

@@ -49,6 +49,17 @@
 #ifndef XA_STAMPS
 #define XA_STAMPS 0
 #endif
+#ifndef XA_WPS
+#define XA_WPS 2  // waves per SIMD the register budget is cut for
+#endif
+#ifndef XA_EXP
+#define XA_EXP 0  // timing-only knockouts (wrong results; tools/ab.sh A/B): 1 scans, 2 state
+                  // corrections, 4 LO products, 8 next-tile loads, 16 output stores, 32 forward pass
+#endif
+#ifndef XA_PF
+#define XA_PF 0   // next-tile load issue points: 0 = 4 groups at the tile start, 2 after the
+                  // forward pass, 2 after the scan; 1 = all 8 after the forward pass
+#endif
 
 namespace zfft {
 namespace xa {
@@ -72,7 +83,7 @@ struct Geo {
   // LDS per wave: the tile transpose (both halves) + FIR carry (12 used) + frame-end v
   // carry (the 64 v before the last tile)
   static constexpr int kBuf = kHalves * kHalfRows * kRow + 16 + 64;
-  static constexpr int kWavesPerSimd = B == 32 ? 2 : 1;  // the register budget is cut for
+  static constexpr int kWavesPerSimd = B == 32 ? XA_WPS : 1;  // the register budget is cut for
 };
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -233,6 +244,7 @@ __device__ __forceinline__ v2f row_shift(v2f src, int d) {  // by 2^d lanes insi
 }
 template <int B, int PASS, bool UP>
 __device__ __forceinline__ void modal_scan(Md &m, CT tab, int lane, v4f xw) {
+  if (XA_EXP & 1) return;
   asm volatile("" : "+v"(lane));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -287,6 +299,7 @@ __device__ __forceinline__ CT after(CT p, v2f v) {
 // read by scalar loads)
 __device__ __forceinline__ v2f add_modal(v2f acc, const float __attribute__((address_space(4))) *row,
                                          const Md &m) {
+  if (XA_EXP & 2) return acc + m.r[0];
 #pragma unroll
   for (int r = 0; r < 8; ++r) acc = vfma(splat(row[r]), m.r[r], acc);
   return acc;
@@ -410,7 +423,9 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       }
 #pragma unroll
       for (int c = 2 * nw; c < kChunks; ++c) vc[c] = hr[c * (64 / K) * kHeldRow];
-      if (inside) {
+      if (inside && (XA_EXP & 16)) {
+        if (vw[0].x == 1.2345f && vc[kChunks - 1].x == 1.2345f) od[0] = vc[kChunks - 1];
+      } else if (inside) {
 #pragma unroll
         for (int c = 0; c < nw; ++c)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vw[c]), orsrc,
@@ -496,6 +511,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   uint32_t next_off = 0;  // byte offset of this lane's (first) element of the next tile's chunk 0
   // next-tile loads: group g = chunks [g kCh/8, (g+1) kCh/8), issued at 8 points of the tile
   auto issue_group = [&](int g) {
+    if ((XA_EXP & 8) && next_i0 > 4 * T) return;
     if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + kSpan * (lane % kCh)];
 #pragma unroll
     for (int q = g * (kCh / 8); q < (g + 1) * (kCh / 8); ++q)
@@ -545,7 +561,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
           for (int q = 0; q < kCh; ++q) {
             // FLIP: the pair was read from descending addresses, so its halves swap
             v2f x0 = cvt_raw<DT>(FLIP ? pf[q].b : pf[q].a), x1 = cvt_raw<DT>(FLIP ? pf[q].a : pf[q].b);
-            if constexpr (MIX) {
+            if constexpr (MIX && !(XA_EXP & 4)) {
               const v2f c = lane_of(cqv, q);  // lane q holds chunk q's start (LDS: 1 % slower)
               x0 = cmul2(x0, cmul2(c, wl0));
               x1 = cmul2(x1, cmul2(c, wl1));
@@ -573,10 +589,12 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     // the next tile's loads: groups 0-3 now, 4-5 after the forward pass, 6-7 after the scan
     // (later issue points leave the register allocator room it does not use: spills; all
     // eight groups at the tile start measured no faster)
-    issue_group(0);
-    issue_group(1);
-    issue_group(2);
-    issue_group(3);
+    if (XA_PF == 0) {
+      issue_group(0);
+      issue_group(1);
+      issue_group(2);
+      issue_group(3);
+    }
     XA_STAMP(0);
 
     // ---- forward all-pole cascade: one pass from a zero state streaming the FIR (v0 -> h
@@ -611,6 +629,11 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
           for (int t = 0; t < 25; ++t) m25s[t] = tbs->m25[t];
 #pragma unroll
           for (int t = 0; t < B; ++t) {
+            if (XA_EXP & 32) {
+              h[t / 2] += y[t];
+              if (t >= 20) s[t & 7] += y[t];
+              continue;
+            }
             const v2f v = ap_step(y[t], s, a1, a2);
             y[t] = v;
 #pragma unroll
@@ -645,8 +668,18 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
           }
         }
         XA_STAMP(1);
+        if (XA_PF == 1) {
+          issue_group(0);
+          issue_group(1);
+          issue_group(2);
+          issue_group(3);
+        }
         issue_group(4);
         issue_group(5);
+        if (XA_PF == 1) {
+          issue_group(6);
+          issue_group(7);
+        }
         fold_entering<0>(m, m_in, tab, ln == 0);
         modal_scan<B, 0, true>(m, tab, ln, xw_l[0][ln & 15]);
 #pragma unroll
@@ -655,8 +688,10 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
         for (int r = 0; r < 8; ++r) m_in.r[r] = lane_of(m.r[r], 63);  // next tile's entering state
       }
       XA_STAMP(2);
-      issue_group(6);
-      issue_group(7);
+      if (XA_PF == 0) {
+        issue_group(6);
+        issue_group(7);
+      }
       // + the entering state's response through the FIR (own outputs, neighbour share);
       // row k's constants are read once output k-4 is done (at most 4 rows in flight)
       // (scalar reads; row k once output k-4 is done: LDS broadcast reads measured 6 % slower)

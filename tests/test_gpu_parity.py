@@ -407,7 +407,8 @@ def test_plan_fed_push_refuses_short_rows():
         with pytest.raises(ValueError):
             plan.waterfall_push()
         plan.waterfall_push(np.full(127, -150.0, np.float32))
-        assert (plan.waterfall_image() == -150.0).all(axis=1).any()
+        # the pushed row, apart from the tick stamps image_update writes (S:1655-1662)
+        assert (plan.waterfall_image() == -150.0).sum(axis=1).max() >= 120
 
 
 def test_xa_refuses_frames_beyond_32bit_offsets():
