@@ -206,6 +206,14 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * auto_xa, use_fused). */
 int zfft_plan_path(zfft_plan *plan, int32_t path);
 
+/* Batched multi-IF (BASELINE config 4): one LO frequency per group of frames in a single
+ * plan and launch chain.  Frame f of every zfft_process* / zfft_decimate call (f counted from
+ * the call's first frame) is mixed with f_lo[(f / frames_per_lo) % n] instead of cfg.f_lo --
+ * the reference's mixer (S:2090-2094) with f_demod per IF.  frames_per_lo = 1 interleaves
+ * the IFs frame by frame; n = 0 restores cfg.f_lo; n = 1 replaces cfg.f_lo.  The LO table
+ * holds n rows of n_samples complex64 (n <= 256).  Waits for the plan's enqueued work. */
+int zfft_plan_set_lo_frames(zfft_plan *plan, const double *f_lo, int32_t n, int32_t frames_per_lo);
+
 /* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 8192, four-step
  * beyond), 1 = one workgroup per frame (n_fft <= 16384), 2 = four-step N1 x 256 (n_fft in
  * [4096, 65536]).  Same rows within the parity gate; diagnostics / A-B only. */

@@ -353,6 +353,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR
   const int f = blockIdx.x * kWaves + wv;
   if (f >= frames) return;  // whole wave
+  if constexpr (MIX) lo = lo_row(lo, in, f);  // this frame's LO (config 4: one per IF)
   const LP buf0 = (LP)lds_all[wv];           // half-tile transposes: 32 rows of kRow v2f
   LP buf = buf0;
   LP pcarry = buf + kHalves * kHalfRows * kRow;  // lane 63's FIR neighbour part, for next lane 0

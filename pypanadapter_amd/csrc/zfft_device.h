@@ -46,6 +46,12 @@ __device__ __forceinline__ v2f load_in_t(const InDesc &d, int64_t f, int64_t i) 
   }
 }
 
+// The LO table row of frame f of a call (InDesc lo_* fields; row 0 for a single f_lo).
+__device__ __forceinline__ const v2f *lo_row(const v2f *lo, const InDesc &d, int64_t f) {
+  if (d.lo_n <= 1) return lo;
+  return lo + (int64_t)((((int64_t)d.lo_first + f) / d.lo_per) % d.lo_n) * d.lo_stride;
+}
+
 __device__ __forceinline__ v2f load_in(const InDesc &d, int64_t f, int64_t i) {
   if (d.dtype == kInC64) return load_in_t<kInC64>(d, f, i);
   if (d.dtype == kInC32H) return load_in_t<kInC32H>(d, f, i);

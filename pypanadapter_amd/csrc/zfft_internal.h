@@ -30,10 +30,15 @@ Sos32 sos32();
 //   3 real float32 (AudioPan's pyaudio paFloat32 stream, S:712-713): I = x, Q = 0.
 // flip fuses the sources' np.flip (S:541-543, 459-460) into the stage-0 loads.
 enum InDtype { kInC64 = 0, kInC32H = 1, kInCU8 = 2, kInF32R = 3 };
+// LO rows (config 4, batched multi-IF): the mixer table holds lo_n rows of lo_stride
+// entries; frame f of a call uses row ((lo_first + f) / lo_per) % lo_n (lo_first: the call's
+// first frame within a batched host call).  One row (the default) = the plan's f_lo.
 struct InDesc {
   const void *p;
   int64_t stride, len;
   int dtype, flip;
+  int64_t lo_stride = 0;
+  int lo_n = 1, lo_per = 1, lo_first = 0;
 };
 inline size_t in_elem_bytes(int dtype) { return dtype == kInC64 ? 8 : (dtype == kInC32H || dtype == kInF32R) ? 4 : 2; }
 

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void iir_forward_fgi_kernel(const v2f *__restr
 constexpr int kTile = 16;
 constexpr int kTileStride = kTile + 2;  // float2 units: 144 B rows, 16 B aligned, conflict-free
 
-template <int DT>
+template <int DT, bool MULTI_LO>
 __global__ __launch_bounds__(256) void iir_forward_mix_kernel(InDesc in, int frames,
                                                               const v2f *__restrict__ lo,
                                                               v2f *__restrict__ yf, StageGeom g,
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(InDesc in, int fra
   const int lrow = w.lane >> 4, lcol = w.lane & 15;
 
   auto xm = [&](int f, int i) -> v2f {  // mixed sample i of the window of frame f
-    return cmul2(load_in_t<DT>(in, f, o + i), lob[i]);
+    return cmul2(load_in_t<DT>(in, f, o + i), (MULTI_LO ? lo_row(lo, in, f) + o : lob)[i]);
   };
   auto ext_slow = [&](int f, int j) -> v2f {
     if (f >= frames || j < 0 || j >= e) return splat(0.f);
@@ -189,7 +189,13 @@ __global__ __launch_bounds__(256) void iir_forward_mix_kernel(InDesc in, int fra
   auto load_tile = [&](int jc) {
     const int j = jc + lcol;
     const bool fast = jc >= kPad && jc + kTile <= n + kPad && f0 + 64 <= frames;  // uniform
-    if (fast) {
+    if (fast && MULTI_LO) {  // config 4: each frame (row) has its own LO row
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int f = f0 + lrow + 4 * q;
+        pf[q] = cmul2(load_in_t<DT>(in, f, o + j - kPad), lo_row(lo, in, f)[o + j - kPad]);
+      }
+    } else if (fast) {
       const v2f l = lob[j - kPad];
 #pragma unroll
       for (int q = 0; q < 16; ++q) pf[q] = cmul2(load_in_t<DT>(in, f0 + lrow + 4 * q, o + j - kPad), l);
@@ -414,7 +420,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(InDesc in, const v2f *__res
   if (k >= total) return;
   const int64_t f = k / in.len, i = k - f * in.len;
   const v2f v = load_in_t<DT>(in, f, i);
-  out[k] = lo ? cmul2(v, lo[i]) : v;
+  out[k] = lo ? cmul2(v, lo_row(lo, in, f)[i]) : v;
 }
 
 // ------------------------------------------------------------------ Welch row
@@ -1197,14 +1203,23 @@ hipError_t launch_iir_forward_mix(const InDesc &in, int frames, const float2 *lo
   const dim3 grid(wave_blocks(g)), block(256);
   const v2f *l = (const v2f *)lo;
   v2f *y = (v2f *)yf;
-  if (in.dtype == kInC64)
-    hipLaunchKernelGGL(iir_forward_mix_kernel<kInC64>, grid, block, 0, st, in, frames, l, y, g, sos32());
+  if (in.lo_n > 1) {
+    if (in.dtype == kInC64)
+      hipLaunchKernelGGL((iir_forward_mix_kernel<kInC64, true>), grid, block, 0, st, in, frames, l, y, g, sos32());
+    else if (in.dtype == kInC32H)
+      hipLaunchKernelGGL((iir_forward_mix_kernel<kInC32H, true>), grid, block, 0, st, in, frames, l, y, g, sos32());
+    else if (in.dtype == kInF32R)
+      hipLaunchKernelGGL((iir_forward_mix_kernel<kInF32R, true>), grid, block, 0, st, in, frames, l, y, g, sos32());
+    else
+      hipLaunchKernelGGL((iir_forward_mix_kernel<kInCU8, true>), grid, block, 0, st, in, frames, l, y, g, sos32());
+  } else if (in.dtype == kInC64)
+    hipLaunchKernelGGL((iir_forward_mix_kernel<kInC64, false>), grid, block, 0, st, in, frames, l, y, g, sos32());
   else if (in.dtype == kInC32H)
-    hipLaunchKernelGGL(iir_forward_mix_kernel<kInC32H>, grid, block, 0, st, in, frames, l, y, g, sos32());
+    hipLaunchKernelGGL((iir_forward_mix_kernel<kInC32H, false>), grid, block, 0, st, in, frames, l, y, g, sos32());
   else if (in.dtype == kInF32R)
-    hipLaunchKernelGGL(iir_forward_mix_kernel<kInF32R>, grid, block, 0, st, in, frames, l, y, g, sos32());
+    hipLaunchKernelGGL((iir_forward_mix_kernel<kInF32R, false>), grid, block, 0, st, in, frames, l, y, g, sos32());
   else
-    hipLaunchKernelGGL(iir_forward_mix_kernel<kInCU8>, grid, block, 0, st, in, frames, l, y, g, sos32());
+    hipLaunchKernelGGL((iir_forward_mix_kernel<kInCU8, false>), grid, block, 0, st, in, frames, l, y, g, sos32());
   return hipGetLastError();
 }
 

@@ -379,7 +379,10 @@ struct zfft_plan {
   DevBuf lo, win, tw, in, in2, yf, ping, pong, rows, ring, img, one_row, dec;
   hipStream_t copy_st = nullptr;            // H2D of the next batch in zfft_process
   hipEvent_t h2d_ev[2] = {}, comp_ev[2] = {};
-  int64_t lo_len = 0;
+  int64_t lo_len = 0;                       // entries per LO row (0: not built)
+  std::vector<double> lo_freqs;             // set_lo_frames: one LO row per entry (config 4)
+  int lo_per = 1;                           // frames per LO row
+  int lo_first = 0;                         // first frame of the current batch (zfft_process)
   int win_len = -1;
   double win_ss = 0.0;
   int block_override = 0, warm_override = 0;
@@ -461,22 +464,29 @@ int quiesce(zfft_plan *p);
 int use_stream(zfft_plan *p, hipStream_t st);
 int done_on(zfft_plan *p, hipStream_t st);
 
+// LO table: one row of lo_len entries per LO frequency (the plan's f_lo, or the
+// zfft_plan_set_lo_frames list), rows lo_len apart.
 int ensure_lo(zfft_plan *p, int64_t L) {
   if (p->lo_len >= L) return ZFFT_OK;
   int rc = quiesce(p);
   if (rc) return rc;
-  int64_t cap = std::max<int64_t>(L, 64);  // the XA kernels read lo[lane] for every lane
-  std::vector<float2> h(cap);
-  const double r = p->cfg.f_lo / p->cfg.fs, sq2 = std::sqrt(2.0);
-  for (int64_t n = 0; n < cap; ++n) {
-    // lo[n] = sqrt(2) exp(-2 pi i f_lo n / fs) on integer n (S:2091-2093)
-    const double turns = std::fmod((double)n * r, 1.0);
-    const double ph = -2.0 * M_PI * turns;
-    h[n] = make_float2((float)(sq2 * std::cos(ph)), (float)(sq2 * std::sin(ph)));
+  // the XA kernels read lo[lane] for every lane; rows 64-entry aligned
+  const int64_t cap = (std::max<int64_t>(L, 64) + 63) & ~(int64_t)63;
+  const std::vector<double> freqs = p->lo_freqs.empty() ? std::vector<double>{p->cfg.f_lo} : p->lo_freqs;
+  std::vector<float2> h(cap * freqs.size());
+  const double sq2 = std::sqrt(2.0);
+  for (size_t k = 0; k < freqs.size(); ++k) {
+    const double r = freqs[k] / p->cfg.fs;
+    for (int64_t n = 0; n < cap; ++n) {
+      // lo[n] = sqrt(2) exp(-2 pi i f_lo n / fs) on integer n (S:2091-2093)
+      const double turns = std::fmod((double)n * r, 1.0);
+      const double ph = -2.0 * M_PI * turns;
+      h[k * cap + n] = make_float2((float)(sq2 * std::cos(ph)), (float)(sq2 * std::sin(ph)));
+    }
   }
-  hipError_t e = p->lo.ensure(cap * sizeof(float2));
+  hipError_t e = p->lo.ensure(h.size() * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "LO table allocation failed");
-  e = hipMemcpy(p->lo.p, h.data(), cap * sizeof(float2), hipMemcpyHostToDevice);
+  e = hipMemcpy(p->lo.p, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "LO table upload");
   p->lo_len = cap;
   return ZFFT_OK;
@@ -564,6 +574,8 @@ int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
   *out = cur;
   return ZFFT_OK;
 }
+
+constexpr int kMaxLoRows = 256;  // LO rows of set_lo_frames (each n_samples x 8 B)
 
 // Edge width (final-stage samples) recomputed exactly, and the exact window length.
 constexpr int kEdge = 384;
@@ -740,7 +752,14 @@ int row_length(const zfft_plan *p) {
 }
 
 InDesc input_of(const zfft_plan *p, const void *d_iq, int64_t L) {
-  return InDesc{d_iq, L, L, p->cfg.in_dtype, p->cfg.flip_input};
+  InDesc d{d_iq, L, L, p->cfg.in_dtype, p->cfg.flip_input};
+  if (p->lo_freqs.size() > 1) {
+    d.lo_stride = p->lo_len;  // (ensure_lo runs before any kernel reads the rows)
+    d.lo_n = (int)p->lo_freqs.size();
+    d.lo_per = p->lo_per;
+    d.lo_first = p->lo_first;
+  }
+  return d;
 }
 
 int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, float *d_rows,
@@ -1011,6 +1030,23 @@ int zfft_plan_path(zfft_plan *p, int32_t path) {
   return ZFFT_OK;
 }
 
+int zfft_plan_set_lo_frames(zfft_plan *p, const double *f_lo, int32_t n, int32_t frames_per_lo) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (n < 0 || n > kMaxLoRows || (n > 0 && (!f_lo || frames_per_lo < 1)))
+    return fail(ZFFT_EINVAL, "set_lo_frames: 0 <= n <= 256 frequencies, frames_per_lo >= 1");
+  for (int i = 0; i < n; ++i)
+    if (!std::isfinite(f_lo[i])) return fail(ZFFT_EINVAL, "set_lo_frames: f_lo must be finite");
+  rc = quiesce(p);  // the old table may still be read by enqueued work
+  if (rc) return rc;
+  p->lo_freqs.assign(f_lo, f_lo + n);
+  if (n == 1) p->cfg.f_lo = f_lo[0];
+  if (n <= 1) p->lo_freqs.clear();
+  p->lo_per = n > 0 ? frames_per_lo : 1;
+  p->lo_len = 0;  // rebuilt by the next call
+  return ZFFT_OK;
+}
+
 int zfft_plan_welch(zfft_plan *p, int32_t mode) {
   if (!p || mode < 0 || mode > 2)
     return fail(ZFFT_EINVAL, "welch mode must be 0 (auto), 1 (one workgroup) or 2 (four-step)");
@@ -1109,7 +1145,9 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
     if (e == hipSuccess && nb > 1) e = hipStreamWaitEvent(p->stream, p->h2d_ev[buf], 0);
     if (e != hipSuccess) return hip_fail(e, "H2D copy");
     if (k > 0) mark(p, p->stream, "batch_wait");
+    p->lo_first = f0;  // batch frame 0 is call frame f0 (its LO row, config 4)
     rc = process_device(p, dst, L, nk, p->rows.as<float>() + (int64_t)f0 * p->cfg.n_win, p->stream);
+    p->lo_first = 0;
     if (rc) return rc;
     if (nb > 1 && (e = hipEventRecord(p->comp_ev[buf], p->stream)) != hipSuccess)
       return hip_fail(e, "event record");

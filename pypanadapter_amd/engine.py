@@ -125,6 +125,16 @@ class ZoomFFT:
         """0 auto, 1 one workgroup per frame (n_fft <= 16384), 2 four-step (n_fft >= 4096)."""
         check(self.lib.zfft_plan_welch(self._plan, int(mode)), "zfft_plan_welch")
 
+    def set_lo_frames(self, f_lo, frames_per_lo: int = 1) -> None:
+        """Batched multi-IF (config 4): frame f of each call is mixed with
+        f_lo[(f // frames_per_lo) % len(f_lo)] (the reference's f_demod per IF, S:2090);
+        an empty list restores the plan's f_lo."""
+        arr = np.ascontiguousarray(f_lo, dtype=np.float64).ravel()
+        check(self.lib.zfft_plan_set_lo_frames(self._plan, arr.ctypes.data_as(ctypes.c_void_p) if arr.size else None,
+                                               int(arr.size), int(frames_per_lo)), "zfft_plan_set_lo_frames")
+        if arr.size == 1:
+            self.f_lo = float(arr[0])
+
     # ---------------------------------------------------------------- DSP
     def _as_iq(self, x) -> np.ndarray:
         """The caller's frames in the plan's input format, C-contiguous; the last axis holds

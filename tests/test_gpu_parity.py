@@ -439,3 +439,74 @@ def test_batched_host_call_times_every_batch_with_one_schedule():
     assert np.all(np.isfinite(rows))
     assert names.count("batch_wait") >= 1, names
     assert names.count("xa_stage_mix") == names.count("batch_wait") + 1, names
+
+
+IF_LOS = [1.0 + k * 150e3 for k in range(8)]  # config 4's IF centre frequencies
+
+
+@pytest.mark.parametrize("path", [1, 2, 3])
+@pytest.mark.parametrize("per", [1, 3])
+def test_lo_per_frame_every_schedule(oracle_lib, path, per):
+    """Config 4 on one plan: 8 IF LOs over one batch, frame f mixed with
+    f_lo[(f // per) % 8], on every decimator schedule, each frame vs the float64 oracle."""
+    from pypanadapter_amd import ZoomFFT
+    F, L = 24, 65536
+    x = _frames(F, L, 1024, 8, 128, seed0=1300)
+    with ZoomFFT(1024, 8, 2.4e6) as plan:
+        plan.set_path(path)
+        plan.set_lo_frames(IF_LOS, per)
+        rows = plan.rows(x)
+        d = plan.decimate(x[5])  # a single-frame call: frame 0 -> f_lo[0]
+        plan.set_lo_frames([])   # back to the plan's f_lo
+        row0 = plan.rows(x[7])
+    for f in range(F):
+        f_lo = IF_LOS[(f // per) % 8]
+        assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, 1024, 8, 128, f_lo=f_lo),
+                         f"path={path} per={per} frame {f}")
+    ref = oracle_lib.zoomfft(x[5], 8, 2.4e6, f_lo=IF_LOS[0])
+    assert np.abs(d - ref).max() / np.abs(ref).max() < 3e-5
+    assert_row_close(row0, oracle_lib.psd_row(x[7], 2.4e6, 1024, 8, 128), "restored f_lo")
+
+
+def test_lo_per_frame_bench_batch(oracle_lib):
+    """Config 4 at the bench's geometry: 8 IFs x 512 frames of cfg2 in one F = 4096 batch on
+    the device (the XA schedule), two frames of every IF vs the oracle at that IF's f_LO."""
+    import torch
+    import bench
+    from pypanadapter_amd import ZoomFFT
+    cfg = bench.CONFIGS["cfg4"]
+    F, L = 4096, cfg["n_fft"] * cfg["n_avg"]
+    dev = torch.device("cuda", 0)
+    x = bench.make_frames(torch, F, L, cfg, dev, 77)
+    rows = torch.empty((F, 512), dtype=torch.float32, device=dev)
+    with ZoomFFT(4096, 8, 2.4e6, n_win=512) as plan:
+        plan.set_lo_frames(IF_LOS, F // 8)
+        plan.set_timing(True)
+        plan.process_device(x.data_ptr(), L, F, rows.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert plan.launch_names()[0] == "xa_stage_mix"
+    host = rows.cpu().numpy()
+    for k in range(8):
+        for f in (512 * k, 512 * k + 511):
+            xf = bench.decoded_host(torch, x, f, "complex64")
+            assert_row_close(host[f], oracle_lib.psd_row(xf, 2.4e6, 4096, 8, 512, f_lo=IF_LOS[k]),
+                             f"IF {k} frame {f}")
+    del x, rows
+    torch.cuda.empty_cache()
+
+
+def test_lo_per_frame_batched_host_call(oracle_lib):
+    """A batched zfft_process call (H2D pipelined batches): frames keep their call index for
+    the LO choice across the batch boundary."""
+    from pypanadapter_amd import ZoomFFT
+    F, L = 1024, 32768
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal((F, L)) + 1j * rng.standard_normal((F, L))).astype(np.complex64)
+    with ZoomFFT(1024, 8, 2.4e6) as plan:
+        plan.set_lo_frames(IF_LOS, 100)
+        plan.set_timing(True)
+        rows = plan.rows(x)
+        assert "batch_wait" in plan.launch_names()
+    for f in (0, 99, 100, 511, 512, 513, 700, 1023):
+        assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, 1024, 8, 128,
+                                                     f_lo=IF_LOS[(f // 100) % 8]), f"frame {f}")
