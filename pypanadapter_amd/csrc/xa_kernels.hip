@@ -43,6 +43,7 @@
 // Numerics: float32, max relative error ~8e-6 of the decimated IQ vs float64 sosfiltfilt
 // (plain float32 sosfiltfilt: ~1e-6); end-to-end rows within 1e-5 dB (tools/xa_proto.py).
 #include <cstddef>
+#include <type_traits>
 
 #include "zfft_device.h"
 
@@ -56,9 +57,16 @@
 #define XA_EXP 0  // timing-only knockouts (wrong results; tools/ab.sh A/B): 1 scans, 2 state
                   // corrections, 4 LO products, 8 next-tile loads, 16 output stores, 32 forward pass
 #endif
+#ifndef XA_PIN
+#define XA_PIN 0  // the FIR neighbour share P accumulated inside the forward pass (v dies at once)
+#endif
+#ifndef XA_NT
+#define XA_NT 3   // cache policy: 1 = nt (streaming) tile loads, 2 = nt output stores
+#endif
 #ifndef XA_PF
 #define XA_PF 0   // next-tile load issue points: 0 = 4 groups at the tile start, 2 after the
-                  // forward pass, 2 after the scan; 1 = all 8 after the forward pass
+                  // forward pass, 2 after the scan; 1 = all 8 after the forward pass;
+                  // 2 = no prefetch: a tile's loads at its own start
 #endif
 
 namespace zfft {
@@ -68,7 +76,10 @@ namespace xa {
 // once: one LDS round trip per direction and tile (two halves in turn: 4 % slower at cfg2).
 // 4-wave workgroups: 2 of them (78 KB of LDS each) fill a CU at 2 waves per SIMD.
 constexpr int kHalfRows = 32;           // rows of one transpose half (32 lanes' sub-blocks)
-constexpr int kHalves = 2;              // transpose halves held in LDS at once
+#ifndef XA_HALVES
+#define XA_HALVES 2
+#endif
+constexpr int kHalves = XA_HALVES;      // input-transpose halves held in LDS at once (1: in turn)
 constexpr int kWaves = 4;               // waves (frames) per workgroup
 constexpr int kLagChunks = kXaLag / 64; // held output chunks of a tile
 
@@ -82,7 +93,10 @@ struct Geo {
   static constexpr int kRowsPerChunk = 64 / B > 0 ? 64 / B : 1;  // input rows one 64-sample chunk fills
   // LDS per wave: the tile transpose (both halves) + FIR carry (12 used) + frame-end v
   // carry (the 64 v before the last tile)
-  static constexpr int kBuf = kHalves * kHalfRows * kRow + 16 + 64;
+  // (the output transpose, 64 rows of kHeldRow, reuses the input transpose's space)
+  static constexpr int kIn = kHalves == 2 ? 2 * kHalfRows * kRow : 64 * (B / 2 + 2);
+  static constexpr int kMain = kIn > 64 * kHeldRow ? kIn : 64 * kHeldRow;
+  static constexpr int kBuf = kMain + 16 + 64;
   static constexpr int kWavesPerSimd = B == 32 ? XA_WPS : 1;  // the register budget is cut for
 };
 
@@ -124,23 +138,30 @@ template <int DT> struct Pair {
 };
 
 // one raw element (or pair) through a buffer resource (out-of-range offsets read 0)
+constexpr int kLoadAux = (XA_NT & 1) ? 2 : 0;   // aux 2 = nt
+constexpr int kStoreAux = (XA_NT & 2) ? 2 : 0;
 template <class T>
 __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   T v;
   if constexpr (sizeof(T) == 16) {
-    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kLoadAux);
     __builtin_memcpy(&v, &u, 16);
   } else if constexpr (sizeof(T) == 8) {
-    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kLoadAux);
     __builtin_memcpy(&v, &u, 8);
   } else if constexpr (sizeof(T) == 4) {
-    const auto u = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    const auto u = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kLoadAux);
     __builtin_memcpy(&v, &u, 4);
   } else {
-    const auto u = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+    const auto u = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, kLoadAux);
     __builtin_memcpy(&v, &u, 2);
   }
   return v;
+}
+
+__device__ __forceinline__ void st_out(v2f *p, v2f v) {  // one output (final, unmasked form)
+  if constexpr (kStoreAux) __builtin_nontemporal_store(v, p);
+  else *p = v;
 }
 
 struct Md {
@@ -356,7 +377,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   if constexpr (MIX) lo = lo_row(lo, in, f);  // this frame's LO (config 4: one per IF)
   const LP buf0 = (LP)lds_all[wv];           // half-tile transposes: 32 rows of kRow v2f
   LP buf = buf0;
-  LP pcarry = buf + kHalves * kHalfRows * kRow;  // lane 63's FIR neighbour part, for next lane 0
+  LP pcarry = buf + G::kMain;  // lane 63's FIR neighbour part, for next lane 0
   LP vcarry = pcarry + 16;                  // the 64 v before the last tile
   const int e = n + 2 * kPad, n_out = (n + 1) >> 1;
   const int nt = (e + 15) / T + 1;  // the last FIR/backward tile reaches e - 1
@@ -430,9 +451,9 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
 #pragma unroll
         for (int c = 0; c < nw; ++c)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vw[c]), orsrc,
-                                                 (uint32_t)(m_of(tile, 128 * c + 2 * ln) * 8), 0, 0);
+                                                 (uint32_t)(m_of(tile, 128 * c + 2 * ln) * 8), 0, kStoreAux);
 #pragma unroll
-        for (int c = 2 * nw; c < kChunks - kLagChunks; ++c) od[64 * c] = vc[c];
+        for (int c = 2 * nw; c < kChunks - kLagChunks; ++c) st_out(od + 64 * c, vc[c]);
       } else {
 #pragma unroll
         for (int c = 0; c < nw; ++c) {
@@ -471,7 +492,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     const bool inside = m_of(tile, (kChunks - kLagChunks) * 64) >= 0 && m_of(tile, kChunks * 64) <= n_out;
     if (inside) {
 #pragma unroll
-      for (int c = 0; c < kLagChunks; ++c) o[m0 + 64 * c] = held[c];
+      for (int c = 0; c < kLagChunks; ++c) st_out(o + m0 + 64 * c, held[c]);
     } else {
 #pragma unroll
       for (int c = 0; c < kLagChunks; ++c) {
@@ -532,11 +553,15 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       LP b = buf0;
       asm volatile("" : "+s"(b));
       buf = b;
-      pcarry = buf + kHalves * kHalfRows * kRow;
+      pcarry = buf + G::kMain;
       vcarry = pcarry + 16;
     }
     const int base = tau * T;
     const bool last = tau == nt - 1;
+    if (XA_PF == 2) {  // this tile's loads at its start (no register prefetch across tiles)
+#pragma unroll
+      for (int g = 0; g < 8; ++g) issue_group(g);
+    }
     v2f y[B];
     {
       const bool fast = fast_tile(base);  // wave-uniform
@@ -554,31 +579,75 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
         }
         __builtin_amdgcn_wave_barrier();
       };
+      // kHalves == 1: the tile goes through LDS as two column halves in turn (columns
+      // 16 hf .. 16 hf + 15 of all 64 rows, row stride kRowH): every lane takes 16 of its
+      // samples per half, so no lane's registers are written under a divergent mask
+      constexpr int kRowH = B / 2 + 2;  // 144-B rows: b128 reads conflict-free per 16 lanes
+      auto read_col_half = [&](int hf) {
+        __builtin_amdgcn_wave_barrier();
+        const LP4 rp = (LP4)(buf + ln * kRowH);
+#pragma unroll
+        for (int t = 0; t < B / 4; ++t) {
+          const v4f w = rp[t];
+          y[hf * (B / 2) + 2 * t] = v2f{w.x, w.y};
+          y[hf * (B / 2) + 2 * t + 1] = v2f{w.z, w.w};
+        }
+        __builtin_amdgcn_wave_barrier();
+      };
+      auto fast_chunk = [&](int q) -> v4f {
+        // FLIP: the pair was read from descending addresses, so its halves swap
+        v2f x0 = cvt_raw<DT>(FLIP ? pf[q].b : pf[q].a), x1 = cvt_raw<DT>(FLIP ? pf[q].a : pf[q].b);
+        if constexpr (MIX && !(XA_EXP & 4)) {
+          const v2f c = lane_of(cqv, q);  // lane q holds chunk q's start (LDS: 1 % slower)
+          x0 = cmul2(x0, cmul2(c, wl0));
+          x1 = cmul2(x1, cmul2(c, wl1));
+        }
+        return v4f{x0.x, x0.y, x1.x, x1.y};
+      };
       if (fast) {
-        {  // the 64 rows lie contiguous (both halves at once): sample s at row s/B, col s%B;
-          // chunk q's pair of lane l is row 4q + l/16, cols 2 (l%16) + {0, 1}: one b128
+        // sample s at row s/B, col s%B; chunk q's pair of lane l is row 4q + l/16, cols
+        // 2 (l%16) + {0, 1}: one b128
+        if constexpr (kHalves == 2) {  // the 64 rows contiguous (both halves at once)
           const LP4 st2 = (LP4)(buf + (ln / 16) * kRow + 2 * (ln % 16));
 #pragma unroll
-          for (int q = 0; q < kCh; ++q) {
-            // FLIP: the pair was read from descending addresses, so its halves swap
-            v2f x0 = cvt_raw<DT>(FLIP ? pf[q].b : pf[q].a), x1 = cvt_raw<DT>(FLIP ? pf[q].a : pf[q].b);
-            if constexpr (MIX && !(XA_EXP & 4)) {
-              const v2f c = lane_of(cqv, q);  // lane q holds chunk q's start (LDS: 1 % slower)
-              x0 = cmul2(x0, cmul2(c, wl0));
-              x1 = cmul2(x1, cmul2(c, wl1));
+          for (int q = 0; q < kCh; ++q) st2[q * (4 * kRow / 2)] = fast_chunk(q);
+          read_all_rows();
+        } else {
+          v4f cx[kCh];
+#pragma unroll
+          for (int q = 0; q < kCh; ++q) cx[q] = fast_chunk(q);
+          // lane l's pair sits in column half (l % 16) / 8, at column 2 (l % 8)
+          const LP4 st2 = (LP4)(buf + (ln / 16) * kRowH + 2 * (ln % 8));
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            if (((ln >> 3) & 1) == hf) {
+#pragma unroll
+              for (int q = 0; q < kCh; ++q) st2[q * (4 * kRowH / 2)] = cx[q];
             }
-            st2[q * (4 * kRow / 2)] = v4f{x0.x, x0.y, x1.x, x1.y};
+            read_col_half(hf);
           }
         }
-        read_all_rows();
       } else {
+        if constexpr (kHalves == 2) {
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
+          for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll 4
-          for (int qq = 0; qq < B / 2; ++qq)
-            st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = ext(base + ln + 64 * (hf * (B / 2) + qq));
+            for (int qq = 0; qq < B / 2; ++qq)
+              st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = ext(base + ln + 64 * (hf * (B / 2) + qq));
+          }
+          read_all_rows();
+        } else {
+          // sample 64 Q + ln: row 2 Q + ln / 32, column ln % 32, in column half (ln % 32) / 16
+          const LP sth = buf + (ln / 32) * kRowH + (ln % 16);
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            if (((ln >> 4) & 1) == hf) {
+#pragma unroll 4
+              for (int Q = 0; Q < B; ++Q) sth[2 * Q * kRowH] = ext(base + ln + 64 * Q);
+            }
+            read_col_half(hf);
+          }
         }
-        read_all_rows();
       }
     }
     next_fast = tau + 1 < nt && fast_tile(base + T);  // wave-uniform
@@ -628,45 +697,63 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
           float m25s[25];
 #pragma unroll
           for (int t = 0; t < 25; ++t) m25s[t] = tbs->m25[t];
-#pragma unroll
-          for (int t = 0; t < B; ++t) {
-            if (XA_EXP & 32) {
-              h[t / 2] += y[t];
-              if (t >= 20) s[t & 7] += y[t];
-              continue;
+          // frame end: the 64 v before the last tile (lanes 64 - 64/B .. 63 of the tile
+          // before it) and the last tile's two lanes around e-25 .. e-1 go to LDS for
+          // f = N v -- v0 during the pass, the entering state's part once it is known.  Those
+          // two tiles run a copy of the pass with the stores; every other tile's pass lets
+          // each v die as soon as it has entered the FIR (own outputs h, neighbour share P).
+          {
+            constexpr bool kStore = true;
+            LP wrow = buf;
+            bool wlane = false;
+            if (tau >= nt - 2) {
+              const int la = max(0, (e - 25 - base) / B);
+              wlane = (!last && ln >= 64 - 64 / B) || (last && (ln == la || ln == la + 1));
+              // (no null test on an LDS pointer: LDS address 0 is this workgroup's first row)
+              wrow = last ? buf + (ln - la) * kRow : vcarry + (ln - (64 - 64 / B)) * B;
             }
-            const v2f v = ap_step(y[t], s, a1, a2);
-            y[t] = v;
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-              const int tap = 24 + t - 1 - 2 * k;
-              if (tap >= 0 && tap < 25) h[k] = vfma(splat(m25s[tap]), v, h[k]);
+            for (int t = 0; t < B; ++t) {
+              if (XA_EXP & 32) {
+                h[t / 2] += y[t];
+                if (t >= 20) s[t & 7] += y[t];
+                continue;
+              }
+              const v2f v = ap_step(y[t], s, a1, a2);
+#pragma unroll
+              for (int k = 0; k < K; ++k) {
+                const int tap = 24 + t - 1 - 2 * k;
+                if (tap >= 0 && tap < 25) h[k] = vfma(splat(m25s[tap]), v, h[k]);
+              }
+              // this lane's share of its right neighbour's outputs: W[m] = v[B - 24 + m],
+              // 1 <= m < 24
+#pragma unroll
+              for (int k = 0; k < 12; ++k) {
+                const int tap = t - (B - 24) - 1 - 2 * k;
+                if (XA_PIN && t >= B - 23 && tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), v, P[k]);
+              }
+              if (!XA_PIN) y[t] = v;
+              if constexpr (kStore) {
+                if (XA_PIN && wlane) wrow[t] = v;
+              }
+            }
+            if (!XA_PIN) {
+#pragma unroll
+              for (int t = B - 23; t < B; ++t) {
+#pragma unroll
+                for (int k = 0; k < 12; ++k) {
+                  const int tap = t - (B - 24) - 1 - 2 * k;
+                  if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), y[t], P[k]);
+                }
+              }
+              if (wlane) {
+                LP4 wp = (LP4)wrow;
+#pragma unroll
+                for (int t = 0; t < B / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
+              }
             }
           }
           to_modal<0>(tab, s, m);
-          // this lane's share of its right neighbour's outputs: W[m] = v[B - 24 + m],
-          // 1 <= m < 24
-#pragma unroll
-          for (int t = B - 23; t < B; ++t) {
-#pragma unroll
-            for (int k = 0; k < 12; ++k) {
-              const int tap = t - (B - 24) - 1 - 2 * k;
-              if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), y[t], P[k]);
-            }
-          }
-          // frame end: the 64 v before the last tile (lanes 64 - 64/B .. 63 of the tile
-          // before it) and the last tile's two lanes around e-25 .. e-1 go to LDS for
-          // f = N v -- v0 now (y dies here), the entering state's part once it is known
-          // (`ln`: an opaque ln id, so these once-per-frame addresses are not hoisted)
-          if (tau >= nt - 2) {
-            const int la = max(0, (e - 25 - base) / B);
-            if ((!last && ln >= 64 - 64 / B) || (last && (ln == la || ln == la + 1))) {
-              // (no null test on an LDS pointer: LDS address 0 is this workgroup's first row)
-              LP4 wp = (LP4)(last ? buf + (ln - la) * kRow : vcarry + (ln - (64 - 64 / B)) * B);
-#pragma unroll
-              for (int t = 0; t < B / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
-            }
-          }
         }
         XA_STAMP(1);
         if (XA_PF == 1) {

@@ -772,6 +772,10 @@ int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, fl
   const int nperseg = (int)(Ld < N ? Ld : N);
   rc = ensure_window(p, nperseg);
   if (rc) return rc;
+  if (p->K > 0) {  // the LO rows exist (and have their stride) before input_of reads it
+    rc = ensure_lo(p, L);
+    if (rc) return rc;
+  }
   const InDesc in = input_of(p, d_iq, L);
   const float2 *x = (const float2 *)d_iq;
   if (p->n_marks == 0) mark(p, st, "start");  // (the entry points reset the marks per call)
