@@ -60,6 +60,7 @@ IN_BYTES = {"complex64": 8, "complex32": 4, "cu8": 2}
 TONES = ((0.31, 1.0), (-0.57, 0.1))
 # plan launch name -> kernel-name prefix in the rocprofv3 / PMC summaries
 KERNEL_OF = {"xa_stage_mix": "xa_stage_kernel<true", "xa_stage": "xa_stage_kernel<false",
+             "xa_fused_mix": "xa_fused_kernel<true", "xa_fused": "xa_fused_kernel<false",
              "welch_rows": "welch_", "welch4": "welch4_"}
 
 
@@ -319,6 +320,8 @@ def main():
     ap.add_argument("--warm", type=int, default=0)
     ap.add_argument("--path", type=int, default=0,
                     help="0 auto, 1 exact order, 2 fused interior, 3 XA tiles")
+    ap.add_argument("--fuse", type=int, default=0,
+                    help="XA stages per launch: 0 auto, 1 one per stage, 2-3 fused (A/B runs)")
     ap.add_argument("--welch", type=int, default=0,
                     help="Welch kernel: 0 auto, 1 one workgroup per frame, 2 four-step (A/B runs)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -396,6 +399,8 @@ def main():
         plan.set_path(args.path)
     if args.welch:
         plan.set_welch(args.welch)
+    if args.fuse:
+        plan.set_fuse(args.fuse)
     stream = torch.cuda.Stream(dev)  # a real stream: the null stream's handle (0) would be
     torch.cuda.set_stream(stream)    # read by the C-ABI as HIP's default stream
     sp = stream.cuda_stream
@@ -485,7 +490,7 @@ def main():
         os.path.join(ROOT, "profiles", f"traffic_{args.config}.json"), F, args.in_dtype)
     sq_j, sq_status = stamped_profile(os.path.join(ROOT, "profiles", f"sq_{args.config}.json"), F,
                                       args.in_dtype)
-    default_sched = not (args.path or args.welch or args.block or args.warm)
+    default_sched = not (args.path or args.welch or args.block or args.warm or args.fuse)
     dom_traffic = step_traffic = valu = None
     if dominant is not None and default_sched:
         pref = KERNEL_OF.get(dominant.split(":", 1)[1], "?")

@@ -742,6 +742,11 @@ constexpr int kDifWavesSmall = 3;      // the same for N <= 2048 (full form)
 constexpr int kDifWavesSmallPrune = 4; // N <= 2048, PRUNE: 4 waves/SIMD (cfg1: 4096 one-wave
                                        // frames fill the GPU's 4096 slots in one round)
 constexpr int kDifPfSmallPrune = 4;    // prefetch of that form (fits 128 VGPRs)
+#ifndef ZFFT_DIF_PF16K
+#define ZFFT_DIF_PF16K 4
+#endif
+constexpr int kDifPf16k = ZFFT_DIF_PF16K;  // N = 16384 (PRUNE; the full form: none): one
+                                            // 1024-thread frame, 4 waves/SIMD (128 VGPRs)
 __host__ __device__ constexpr int dif_slot(int i) { return i + (i >> 4); }  // conflict-free strides 1, 16, 17
 
 template <int N>
@@ -756,8 +761,8 @@ struct Dif {
   static constexpr int NT = T * FPB;                 // threads per workgroup
   static constexpr int NW = (T + 63) / 64;           // waves per frame
   static constexpr int SLOTS = dif_slot(N - 1) + 1;  // LDS image per frame (v2f)
-  static constexpr int PF = N <= 2048 ? kDifPfSmall : kDifPf;
-  static constexpr int PF_PRUNE = N <= 2048 ? kDifPfSmallPrune : kDifPf;
+  static constexpr int PF = N <= 2048 ? kDifPfSmall : N == 16384 ? 0 : kDifPf;
+  static constexpr int PF_PRUNE = N <= 2048 ? kDifPfSmallPrune : N == 16384 ? kDifPf16k : kDifPf;
   // waves per SIMD the registers are cut for
   static constexpr int WAVES_PRUNE = N <= 2048 ? kDifWavesSmallPrune : N == 4096 ? kDifWaves : 2;
   static constexpr int WAVES_FULL = N <= 2048 ? kDifWavesSmall : 2;
@@ -1298,9 +1303,12 @@ static hipError_t welch_launch_t(const float2 *x, int64_t len, const float *win,
   return hipGetLastError();
 }
 
-// the in-place DIF kernel covers 1024 <= N <= 8192 (N = 16384 as one 1024-thread frame
-// spills: four-step by default there)
-constexpr int kDifMin = 1024, kDifMax = 8192;
+// the in-place DIF kernel covers 1024 <= N <= 16384 (N = 16384: one 1024-thread frame per
+// workgroup, 139 KB of LDS, a 4-value prefetch to stay within 128 VGPRs)
+#ifndef ZFFT_DIF_MAX
+#define ZFFT_DIF_MAX 16384
+#endif
+constexpr int kDifMin = 1024, kDifMax = ZFFT_DIF_MAX;
 template <int R0>
 static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
                                const WelchGeom &g, float *rows, int frames, hipStream_t st) {
@@ -1310,6 +1318,7 @@ static hipError_t welch_launch(const float2 *x, int64_t len, const float *win, c
       case 2048: return welch_dif_launch<2048>(x, len, win, tw, g, rows, frames, st);
       case 4096: return welch_dif_launch<4096>(x, len, win, tw, g, rows, frames, st);
       case 8192: return welch_dif_launch<8192>(x, len, win, tw, g, rows, frames, st);
+      case 16384: return welch_dif_launch<16384>(x, len, win, tw, g, rows, frames, st);
       default: break;
     }
   }

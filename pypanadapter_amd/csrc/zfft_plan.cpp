@@ -399,7 +399,8 @@ struct zfft_plan {
   int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows,
                 // 3 XA tiles (all-pole + FIR + half-rate all-pole)
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
-  DevBuf edge, xk, xa_tab, tws, means, z4;
+  DevBuf edge, xk, xa_tab, tws, means, z4, xa_ring;
+  int xa_fuse = 0;  // XA stages per launch (0 auto: kXaFuseAuto)
   // waterfall rendering: colormap LUT (host copy + device), levels
   uint8_t lut[256 * 4] = {};
   bool lut_ready = false;         // lut holds the chosen map (built on first use)
@@ -575,6 +576,15 @@ int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
   return ZFFT_OK;
 }
 
+#ifndef ZFFT_WELCH_ONEWG_MAX
+#define ZFFT_WELCH_ONEWG_MAX 16384
+#endif
+constexpr int kWelchOneWgMax = ZFFT_WELCH_ONEWG_MAX;  // auto Welch: one workgroup per frame up to here
+constexpr int kXaFuseAuto = 1;   // XA stages per launch by default (measured: DESIGN §3.1)
+#ifndef ZFFT_XA_FUSED_D1
+#define ZFFT_XA_FUSED_D1 0
+#endif
+constexpr bool kXaFusedD1 = ZFFT_XA_FUSED_D1;  // diagnostic build: single stages on the fused kernel
 constexpr int kMaxLoRows = 256;  // LO rows of set_lo_frames (each n_samples x 8 B)
 
 // Edge width (final-stage samples) recomputed exactly, and the exact window length.
@@ -703,21 +713,34 @@ int run_fused(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   return ZFFT_OK;
 }
 
-// XA path: one kernel per stage, one wave per frame, stage outputs natural layout.
+// XA path: one wave per frame; groups of up to `fuse` consecutive stages per launch (stages
+// inside a group hand over through per-frame rings), group outputs in natural layout.
 int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t> &n,
            const float2 **out, hipStream_t st) {
+  const int fuse = std::min(p->K, p->xa_fuse > 0 ? p->xa_fuse : kXaFuseAuto);
   hipError_t e = p->ping.ensure((size_t)frames * n[1] * sizeof(float2));
-  if (e == hipSuccess && p->K > 1) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
+  if (e == hipSuccess && p->K > fuse) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
+  if (e == hipSuccess && fuse > 1)
+    e = p->xa_ring.ensure((size_t)frames * (fuse - 1) * kXaRing * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   const float2 *cur = nullptr;
-  for (int k = 0; k < p->K; ++k) {
-    float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
+  for (int k = 0, g = 0; k < p->K; ++g) {
+    const int D = std::min(fuse, p->K - k);
+    float2 *dst = (g & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
     const InDesc src = k == 0 ? in : InDesc{cur, n[k], n[k], kInC64, 0};
-    e = launch_xa_stage(src, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
-                        p->xa_tab.as<XaTab>(), st);
-    if (e != hipSuccess) return hip_fail(e, "xa_stage launch");
-    mark(p, st, k == 0 ? "xa_stage_mix" : "xa_stage");
+    if (D == 1 && !kXaFusedD1) {
+      e = launch_xa_stage(src, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
+                          p->xa_tab.as<XaTab>(), st);
+      if (e != hipSuccess) return hip_fail(e, "xa_stage launch");
+      mark(p, st, k == 0 ? "xa_stage_mix" : "xa_stage");
+    } else {
+      e = launch_xa_fused(src, D, &n[k], p->lo.as<float2>(), k == 0, p->xa_ring.as<float2>(), dst,
+                          frames, p->xa_tab.as<XaTab>(), st);
+      if (e != hipSuccess) return hip_fail(e, "xa_fused launch");
+      mark(p, st, k == 0 ? "xa_fused_mix" : "xa_fused");
+    }
     cur = dst;
+    k += D;
   }
   *out = cur;
   return ZFFT_OK;
@@ -804,9 +827,9 @@ int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, fl
     w.row_a = N / 2 - p->cfg.n_win / 2;
     w.row_len = row_length(p);
   }
-  // auto: four-step above 8192 (cfg3, N = 16384: 1.86 ms against 2.20 for one workgroup
-  // per frame, MI355X); it is the only form above kMaxLdsFft
-  const bool four = p->welch == 2 || (p->welch == 0 && N > 8192);
+  // auto: four-step above 16384 (the only form there); N <= 16384 runs one workgroup per
+  // frame (the in-place DIF kernel from N = 1024)
+  const bool four = p->welch == 2 || (p->welch == 0 && N > kWelchOneWgMax);
   hipError_t e;
   if (four) {
     e = p->means.ensure((size_t)frames * w.nseg * sizeof(float2));
@@ -987,7 +1010,7 @@ int zfft_plan_destroy(zfft_plan *p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->in2, &p->yf, &p->ping, &p->pong, &p->rows,
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
-                    &p->tws, &p->means, &p->z4})
+                    &p->tws, &p->means, &p->z4, &p->xa_ring})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->done_ev) (void)hipEventDestroy(p->done_ev);
@@ -1031,6 +1054,13 @@ int zfft_plan_path(zfft_plan *p, int32_t path) {
   if (!p || path < 0 || path > 3)
     return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused) or 3 (XA tiles)");
   p->path = path;
+  return ZFFT_OK;
+}
+
+int zfft_plan_fuse(zfft_plan *p, int32_t stages) {
+  if (!p || stages < 0 || stages > 3)
+    return fail(ZFFT_EINVAL, "fuse must be 0 (auto) or 1..3 decimation stages per XA launch");
+  p->xa_fuse = stages;
   return ZFFT_OK;
 }
 

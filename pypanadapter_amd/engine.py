@@ -121,6 +121,10 @@ class ZoomFFT:
         frame; auto for >= 1024 frames, or >= 512 frames of <= 2^19 samples)."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
 
+    def set_fuse(self, stages: int) -> None:
+        """XA decimation stages per launch: 0 auto, 1 one launch per stage, 2-3 fused (rings)."""
+        check(self.lib.zfft_plan_fuse(self._plan, int(stages)), "zfft_plan_fuse")
+
     def set_welch(self, mode: int) -> None:
         """0 auto, 1 one workgroup per frame (n_fft <= 16384), 2 four-step (n_fft >= 4096)."""
         check(self.lib.zfft_plan_welch(self._plan, int(mode)), "zfft_plan_welch")

@@ -359,8 +359,9 @@ def test_auto_schedule_by_batch(F, L, want):
         plan.process_device(x.data_ptr(), L, F, rows.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         names = plan.launch_names()
-    first = {"exact": "exact_forward_mix", "fused": "exact_forward_mix", "xa": "xa_stage_mix"}[want]
-    assert names[0] == first, names
+    first = {"exact": ("exact_forward_mix",), "fused": ("exact_forward_mix",),
+             "xa": ("xa_stage_mix", "xa_fused_mix")}[want]
+    assert names[0] in first, names
     assert ("edge_windows" in names) == (want == "fused"), names
     del x, rows
     torch.cuda.empty_cache()
@@ -438,7 +439,7 @@ def test_batched_host_call_times_every_batch_with_one_schedule():
         names = plan.launch_names()
     assert np.all(np.isfinite(rows))
     assert names.count("batch_wait") >= 1, names
-    assert names.count("xa_stage_mix") == names.count("batch_wait") + 1, names
+    assert names.count("xa_fused_mix") == names.count("batch_wait") + 1, names
 
 
 IF_LOS = [1.0 + k * 150e3 for k in range(8)]  # config 4's IF centre frequencies
@@ -484,7 +485,7 @@ def test_lo_per_frame_bench_batch(oracle_lib):
         plan.set_timing(True)
         plan.process_device(x.data_ptr(), L, F, rows.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-        assert plan.launch_names()[0] == "xa_stage_mix"
+        assert plan.launch_names()[0] == "xa_fused_mix"
     host = rows.cpu().numpy()
     for k in range(8):
         for f in (512 * k, 512 * k + 511):
@@ -510,3 +511,50 @@ def test_lo_per_frame_batched_host_call(oracle_lib):
     for f in (0, 99, 100, 511, 512, 513, 700, 1023):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, 1024, 8, 128,
                                                      f_lo=IF_LOS[(f // 100) % 8]), f"frame {f}")
+
+
+@pytest.mark.parametrize("z", [4, 8, 32])
+def test_xa_fused_stages_match_stagewise(oracle_lib, z):
+    """XA with 2-3 decimation stages per launch (per-frame rings between them) against one
+    launch per stage: the same filter arithmetic, rounded differently in places (the two
+    kernels are compiled separately: a few products contract differently), so the forms agree
+    to fp32 rounding (measured <= 1.8e-6 x peak; bound 4e-6 log2(zoom)), and every form
+    against the float64 oracle within XA's tolerance, at
+    lengths around the tile geometry (an intermediate stage shorter than one tile, ragged
+    ends, long frames)."""
+    from pypanadapter_amd import ZoomFFT
+    rng = np.random.default_rng(700 + z)
+    for L in [28 * z, 2048 * 2 + 77, 9000, 65536 + 3, 299008]:
+        x = (rng.standard_normal(L) + 1j * rng.standard_normal(L)).astype(np.complex64)
+        got = {}
+        for fuse in (1, 2, 3):
+            with ZoomFFT(1024, z, 2.4e6) as plan:
+                plan.set_path(3)
+                plan.set_fuse(fuse)
+                got[fuse] = plan.decimate(x)
+        ref = oracle_lib.zoomfft(x, z, 2.4e6)
+        pk = np.abs(ref).max()
+        for fuse in (1, 2, 3):
+            assert got[fuse].shape == ref.shape
+            d = np.abs(got[fuse] - got[1]).max() / pk
+            assert d <= 4e-6 * np.log2(z), (L, z, fuse, float(d))
+            err = np.abs(got[fuse] - ref).max() / pk
+            assert err < 1e-5 * np.log2(z), (L, z, fuse, float(err))
+
+
+def test_xa_fused_batch_rows(oracle_lib):
+    """A batch through the fused XA launch (cfg2 geometry, 24 frames, 8 IF LOs): rows within
+    1e-4 dB of the stage-wise launches and within the gate against the oracle."""
+    from pypanadapter_amd import ZoomFFT
+    x = _frames(24, 299008, 4096, 8, 512, seed0=2400)
+    out = {}
+    for fuse in (1, 3):
+        with ZoomFFT(4096, 8, 2.4e6) as plan:
+            plan.set_path(3)
+            plan.set_fuse(fuse)
+            plan.set_lo_frames(IF_LOS, 3)
+            out[fuse] = plan.rows(x)
+    np.testing.assert_allclose(out[3], out[1], rtol=0, atol=1e-4)
+    for f in (0, 5, 23):
+        assert_row_close(out[3][f], oracle_lib.psd_row(x[f], 2.4e6, 4096, 8, 512, f_lo=IF_LOS[(f // 3) % 8]),
+                         f"frame {f}")

@@ -1,3 +1,4 @@
 set -u
+TESTK="-x -k fused" bash tools/gpu_session.sh r03h tests_k || exit $?
 V=pypanadapter_amd/lib/variants
-AB_REPS=2 bash tools/ab.sh r03f_ko base=default ko39=$V/libzfft_ko39.so ko24=$V/libzfft_ko24.so ko63=$V/libzfft_ko63.so ko7=$V/libzfft_ko7.so
+AB_REPS=2 bash tools/ab.sh r03h_ab base=default fd1=$V/libzfft_fd1.so
