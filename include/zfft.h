@@ -192,10 +192,11 @@ int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *coun
 /* Comma-separated names of the intervals zfft_plan_timings returns (owned by the plan). */
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
-/* Decimator schedule: 0 = automatic (3 for batches of >= 1024 frames, or >= 512 frames of
+/* Decimator schedule: 0 = automatic (3 for batches of >= 768 frames, or >= 384 frames of
  * <= 2^19 samples -- a batched zfft_process call is judged by its whole frame count;
- * otherwise 2 for batches of >= 2^28 samples whose frames are long enough for the edge
- * windows, else 1 -- e.g. one frame per call, the reference's use),
+ * otherwise 2 for batches of >= 2^27 samples whose frames are long enough for the edge
+ * windows, else 1 -- e.g. one frame per call, the reference's use; crossovers measured by
+ * tools/sweep_schedule.py),
  * 1 = blocked warm-up passes in the reference order (frames split over many waves),
  * 2 = blocked, fused commuted-order interior + exact edge windows, 3 = XA tiles (one wave per
  * frame and stage: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned;

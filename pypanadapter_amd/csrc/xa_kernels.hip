@@ -63,6 +63,9 @@
 #ifndef XA_NT
 #define XA_NT 3   // cache policy: 1 = nt (streaming) tile loads, 2 = nt output stores
 #endif
+#ifndef XA_DEFER
+#define XA_DEFER 1  // an inside tile's output stores issued after the next tile's input wait
+#endif
 #ifndef XA_PF
 #define XA_PF 0   // next-tile load issue points: 0 = 4 groups at the tile start, 2 after the
                   // forward pass, 2 after the scan; 1 = all 8 after the forward pass;
@@ -420,6 +423,32 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   v2f held[kLagChunks];
 #pragma unroll
   for (int c = 0; c < kLagChunks; ++c) held[c] = splat(0.f);
+  // XA_DEFER: an inside tile's stores wait in registers until the next tile has consumed its
+  // prefetched input.  vmcnt counts loads and stores in issue order, and the compiler's wait
+  // for the last prefetched chunk at the tile start is vmcnt(0): stores issued at the end of
+  // a tile would be waited for there; issued after that wait and before the next tile's loads
+  // they are long complete by the time those loads are waited for.
+  constexpr int nwD = (kChunks - kLagChunks) / 2, ncD = kChunks - kLagChunks - 2 * nwD;
+  v4f dw[nwD > 0 ? nwD : 1];
+  v2f dc[ncD > 0 ? ncD : 1], dh[kLagChunks];
+  int d_tile = -1, d_held = -1;  // tile of the pending flush / of the pending held outputs
+  auto issue_deferred = [&](int ln) {
+    if (d_held >= 0) {
+      const int m0 = m_of(d_held, (kChunks - kLagChunks) * 64 + ln);
+#pragma unroll
+      for (int c = 0; c < kLagChunks; ++c) st_out(o + m0 + 64 * c, dh[c]);
+      d_held = -1;
+    }
+    if (d_tile >= 0) {
+#pragma unroll
+      for (int c = 0; c < nwD; ++c)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, dw[c]), orsrc,
+                                               (uint32_t)(m_of(d_tile, 128 * c + 2 * ln) * 8), 0, kStoreAux);
+#pragma unroll
+      for (int c = 0; c < ncD; ++c) st_out(o + m_of(d_tile, ln) + 64 * (2 * nwD + c), dc[c]);
+      d_tile = -1;
+    }
+  };
   auto flush_tile = [&](int tile, const v2f *h, int ln) {
     const int m0 = m_of(tile, ln);
     v2f *__restrict__ od = o + m0;
@@ -447,6 +476,12 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       for (int c = 2 * nw; c < kChunks; ++c) vc[c] = hr[c * (64 / K) * kHeldRow];
       if (inside && (XA_EXP & 16)) {
         if (vw[0].x == 1.2345f && vc[kChunks - 1].x == 1.2345f) od[0] = vc[kChunks - 1];
+      } else if (inside && XA_DEFER) {
+#pragma unroll
+        for (int c = 0; c < nw; ++c) dw[c] = vw[c];
+#pragma unroll
+        for (int c = 2 * nw; c < kChunks - kLagChunks; ++c) dc[c - 2 * nw] = vc[c];
+        d_tile = tile;
       } else if (inside) {
 #pragma unroll
         for (int c = 0; c < nw; ++c)
@@ -490,7 +525,11 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     }
     // wave-uniform: every held output of the tile inside the frame -> unconditional stores
     const bool inside = m_of(tile, (kChunks - kLagChunks) * 64) >= 0 && m_of(tile, kChunks * 64) <= n_out;
-    if (inside) {
+    if (inside && XA_DEFER && q != nullptr) {
+#pragma unroll
+      for (int c = 0; c < kLagChunks; ++c) dh[c] = held[c];
+      d_held = tile;
+    } else if (inside) {
 #pragma unroll
       for (int c = 0; c < kLagChunks; ++c) st_out(o + m0 + 64 * c, held[c]);
     } else {
@@ -650,6 +689,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
         }
       }
     }
+    if (XA_DEFER) issue_deferred(ln);
     next_fast = tau + 1 < nt && fast_tile(base + T);  // wave-uniform
     next_i0 = base + T - kPad;
     {  // (FLIP: the pair's elements i0, i0 + 1 sit at len-1-i0 and len-2-i0)
@@ -919,6 +959,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     flush_tile(tau, h, ln);
     XA_STAMP(9);
   }
+  if (XA_DEFER) issue_deferred(lane);
   finish_held(nt - 1, nullptr, nullptr, lane);  // the last tile's top state was exact
 #if XA_STAMPS
   if (lane == 0) {

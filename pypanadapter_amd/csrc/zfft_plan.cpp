@@ -580,6 +580,10 @@ int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
 #define ZFFT_WELCH_ONEWG_MAX 16384
 #endif
 constexpr int kWelchOneWgMax = ZFFT_WELCH_ONEWG_MAX;  // auto Welch: one workgroup per frame up to here
+#ifndef ZFFT_WELCH4_CHUNK_MB
+#define ZFFT_WELCH4_CHUNK_MB 0  // chunks of 48/96/192 MB measured 3.1x/1.8x/1.4x slower (cfg5)
+#endif
+constexpr size_t kWelch4ChunkBytes = (size_t)ZFFT_WELCH4_CHUNK_MB << 20;  // 0: one launch set
 constexpr int kXaFuseAuto = 1;   // XA stages per launch by default (measured: DESIGN §3.1)
 #ifndef ZFFT_XA_FUSED_D1
 #define ZFFT_XA_FUSED_D1 0
@@ -591,12 +595,13 @@ constexpr int kMaxLoRows = 256;  // LO rows of set_lo_frames (each n_samples x 8
 constexpr int kEdge = 384;
 int64_t edge_window(int K) { return ((int64_t)1 << K) * (kEdge + 640); }
 
-// Auto choice between XA (one wave per frame) and the blocked schedules, measured on
-// MI355X: XA needs >= 1024 waves to cover 2 waves x 1024 SIMDs well enough;
-// at 512 frames it still wins for ~300k-sample frames (2.21 vs 2.66 ms, cfg2) but loses for
-// 1M-sample frames (9.12 vs 8.38 ms, cfg5), whose blocked launch has 4x the blocks.
-constexpr int kXaMinFrames = 1024;
-constexpr int kXaMinFramesShort = 512;
+// Auto choice between XA (one wave per frame) and the blocked schedules, from the sweep
+// tools/sweep_schedule.py (profiles/r03i/sweep_schedule.json: ms per call, N = 4096, zoom 8):
+// XA needs enough frames to fill 2 waves x 1024 SIMDs; for ~300k-sample frames it is the
+// fastest from 384 frames (1.66 ms against 1.80 fused / 1.83 exact; 256 frames: 1.62 against
+// 1.25 exact), for 2^20-sample frames from 768 (5.67 against 7.69 fused; 512: 5.56 against 5.28).
+constexpr int kXaMinFrames = 768;
+constexpr int kXaMinFramesShort = 384;
 constexpr int64_t kXaShortFrame = (int64_t)1 << 19;
 // zfft_process pipelining: inputs of >= 64 MB go in batches of about 1 GB (at least two).
 constexpr size_t kPipeMinBytes = (size_t)64 << 20;
@@ -613,10 +618,10 @@ bool xa_fits(const zfft_plan *p, int64_t L) {
 
 // The fused blocked schedule (path 2) saves passes over the frame interior but adds the
 // exact edge-window runs, whose launches cost about as much as a whole pass over a few
-// frames: it wins only for large batches.  Measured on MI355X (frames x samples, ms, path 1
-// / path 2): cfg2 1 x 299008 0.46 / 0.94, 64 x 0.51 / 0.95, 256 x 1.19 / 1.52; cfg1 256 x
-// 262144 1.30 / 1.32; cfg5 64 x 1048576 1.11 / 1.41, 256 x 4.12 / 3.68.
-constexpr int64_t kFusedMinSamples = (int64_t)1 << 28;  // per call
+// frames: it wins only for large batches.  Same sweep (frames x samples, ms, path 1 / path 2):
+// 2^20-sample frames 64: 1.15 / 1.33, 128: 2.20 / 2.04, 256: 4.04 / 3.30; ~300k-sample frames
+// 256: 1.25 / 1.43 (and from 384 frames XA beats both).
+constexpr int64_t kFusedMinSamples = (int64_t)1 << 27;  // per call
 bool use_fused(const zfft_plan *p, int64_t L, int frames) {
   if (p->path == 1 || p->K < 2) return false;
   if (8 * edge_window(p->K) > L) return false;  // windows cost <= 1/4 of a frame
@@ -832,12 +837,23 @@ int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, fl
   const bool four = p->welch == 2 || (p->welch == 0 && N > kWelchOneWgMax);
   hipError_t e;
   if (four) {
-    e = p->means.ensure((size_t)frames * w.nseg * sizeof(float2));
-    if (e == hipSuccess) e = p->z4.ensure((size_t)frames * w.nseg * N * sizeof(float2));
+    // frames in chunks whose intermediate Z (nseg x N complex64 per frame) stays in the
+    // 256 MB Infinity Cache between the column and the row pass instead of round-tripping
+    // through HBM
+    const size_t zf = (size_t)w.nseg * N * sizeof(float2);
+    const int chunk = kWelch4ChunkBytes > 0
+                          ? (int)std::max<size_t>(1, std::min<size_t>(frames, kWelch4ChunkBytes / zf))
+                          : frames;
+    e = p->means.ensure((size_t)chunk * w.nseg * sizeof(float2));
+    if (e == hipSuccess) e = p->z4.ensure((size_t)chunk * zf);
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "four-step Welch workspace allocation failed");
-    e = launch_welch4(x, Ld, p->win.as<float>(), p->tw.as<float2>(), p->tws.as<float2>(), w,
-                      p->means.as<float2>(), p->z4.as<float2>(), d_rows, frames, st);
-    if (e != hipSuccess) return hip_fail(e, "welch4 launch");
+    for (int f0 = 0; f0 < frames; f0 += chunk) {
+      const int nf = std::min(chunk, frames - f0);
+      e = launch_welch4(x + (int64_t)f0 * Ld, Ld, p->win.as<float>(), p->tw.as<float2>(),
+                        p->tws.as<float2>(), w, p->means.as<float2>(), p->z4.as<float2>(),
+                        d_rows + (int64_t)f0 * p->cfg.n_win, nf, st);
+      if (e != hipSuccess) return hip_fail(e, "welch4 launch");
+    }
     mark(p, st, "welch4");
   } else {
     e = launch_welch_rows(x, Ld, p->win.as<float>(), p->tw.as<float2>(), w, d_rows, frames, st);

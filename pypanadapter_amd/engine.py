@@ -116,9 +116,9 @@ class ZoomFFT:
 
     def set_path(self, path: int) -> None:
         """0 auto, 1 exact reference pass order (blocked; the auto choice for small batches,
-        e.g. one frame per call), 2 fused interior + exact edges (blocked; auto from 2^28
+        e.g. one frame per call), 2 fused interior + exact edges (blocked; auto from 2^27
         samples per call), 3 XA tiles (all-pole + FIR + half-rate all-pole, one wave per
-        frame; auto for >= 1024 frames, or >= 512 frames of <= 2^19 samples)."""
+        frame; auto for >= 768 frames, or >= 384 frames of <= 2^19 samples)."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
 
     def set_fuse(self, stages: int) -> None:

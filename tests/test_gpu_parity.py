@@ -341,13 +341,16 @@ def test_facade_matches_reference_rows():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F,L,want", [(1, 299008, "exact"), (64, 1048576, "exact"),
-                                      (256, 1048576, "fused"), (1024, 299008, "xa")])
+@pytest.mark.parametrize("F,L,want", [(1, 299008, "exact"), (256, 299008, "exact"),
+                                      (384, 299008, "xa"), (64, 1048576, "exact"),
+                                      (128, 1048576, "fused"), (512, 1048576, "fused"),
+                                      (768, 1048576, "xa")])
 def test_auto_schedule_by_batch(F, L, want):
     """The automatic decimator schedule follows the measured crossovers (zfft_plan.cpp
-    auto_xa / use_fused): one frame per call -- the reference's use -- and small batches run
-    the exact blocked passes, only batches of >= 2^28 samples the fused interior with edge
-    windows, and >= 1024 frames the XA tiles."""
+    auto_xa / use_fused, tools/sweep_schedule.py): one frame per call -- the reference's use --
+    and small batches run the exact blocked passes, batches of >= 2^27 samples the fused
+    interior with edge windows, and >= 384 frames of <= 2^19 samples (768 of longer ones)
+    the XA tiles."""
     import torch
     from pypanadapter_amd import ZoomFFT
     dev = torch.device("cuda", 0)
