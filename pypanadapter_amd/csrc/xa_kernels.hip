@@ -64,7 +64,7 @@
 #define XA_NT 3   // cache policy: 1 = nt (streaming) tile loads, 2 = nt output stores
 #endif
 #ifndef XA_DEFER
-#define XA_DEFER 1  // an inside tile's output stores issued after the next tile's input wait
+#define XA_DEFER 0  // 1: an inside tile's output stores issued after the next tile's input wait
 #endif
 #ifndef XA_PF
 #define XA_PF 0   // next-tile load issue points: 0 = 4 groups at the tile start, 2 after the

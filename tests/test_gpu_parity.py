@@ -442,7 +442,7 @@ def test_batched_host_call_times_every_batch_with_one_schedule():
         names = plan.launch_names()
     assert np.all(np.isfinite(rows))
     assert names.count("batch_wait") >= 1, names
-    assert names.count("xa_fused_mix") == names.count("batch_wait") + 1, names
+    assert names.count("xa_stage_mix") == names.count("batch_wait") + 1, names
 
 
 IF_LOS = [1.0 + k * 150e3 for k in range(8)]  # config 4's IF centre frequencies
@@ -488,7 +488,7 @@ def test_lo_per_frame_bench_batch(oracle_lib):
         plan.set_timing(True)
         plan.process_device(x.data_ptr(), L, F, rows.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-        assert plan.launch_names()[0] == "xa_fused_mix"
+        assert plan.launch_names()[0] == "xa_stage_mix"
     host = rows.cpu().numpy()
     for k in range(8):
         for f in (512 * k, 512 * k + 511):
