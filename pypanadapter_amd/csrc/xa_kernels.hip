@@ -55,7 +55,8 @@
 #endif
 #ifndef XA_EXP
 #define XA_EXP 0  // timing-only knockouts (wrong results; tools/ab.sh A/B): 1 scans, 2 state
-                  // corrections, 4 LO products, 8 next-tile loads, 16 output stores, 32 forward pass
+                  // corrections, 4 LO products, 8 next-tile loads, 16 output stores, 32 forward pass,
+                  // 64 frame-end tiles loaded as fast tiles
 #endif
 #ifndef XA_PIN
 #define XA_PIN 0  // the FIR neighbour share P accumulated inside the forward pass (v dies at once)
@@ -548,7 +549,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   // are then dead between their use at the tile start and their reload
   typedef typename Raw<DT>::T RawT;
   const RawT *__restrict__ src = (const RawT *)in.p + (int64_t)f * in.stride;
-  auto fast_tile = [&](int b) { return b >= kPad && b + T <= n + kPad; };
+  auto fast_tile = [&](int b) { return b >= kPad && ((XA_EXP & 64) || b + T <= n + kPad); };
   // chunk q = samples 128 q + 2 lane + {0, 1}: a pair per lane (16 B for complex64; one
   // element per lane measured 4.5 % slower at stage 0)
   constexpr int kPer = 2;           // elements per lane and chunk
@@ -699,11 +700,17 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     // the next tile's loads: groups 0-3 now, 4-5 after the forward pass, 6-7 after the scan
     // (later issue points leave the register allocator room it does not use: spills; all
     // eight groups at the tile start measured no faster)
-    if (XA_PF == 0) {
+    if (XA_PF == 0 || XA_PF == 4) {
       issue_group(0);
       issue_group(1);
       issue_group(2);
       issue_group(3);
+    }
+    if (XA_PF == 4) {  // all eight groups at the tile start
+      issue_group(4);
+      issue_group(5);
+      issue_group(6);
+      issue_group(7);
     }
     XA_STAMP(0);
 
@@ -802,8 +809,10 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
           issue_group(2);
           issue_group(3);
         }
-        issue_group(4);
-        issue_group(5);
+        if (XA_PF != 4) {
+          issue_group(4);
+          issue_group(5);
+        }
         if (XA_PF == 1) {
           issue_group(6);
           issue_group(7);

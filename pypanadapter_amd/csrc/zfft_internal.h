@@ -141,6 +141,9 @@ struct WelchGeom {
   // doubled except 0 and N/2, then the reference's fftshift of those N/2+1 bins and its
   // [N/2 - W/2, N/2 + W/2) slice -- row_len = that slice's length, from row_a
   int onesided = 0, row_a = 0, row_len = 0;
+  // four-step only: the column pass leaves per-column-group partial sums of each segment and
+  // the row pass subtracts mean * FFT(window) after the transform (nperseg == n_fft)
+  int fused_mean = 0;
 };
 
 hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, const float2 *tw,
@@ -149,8 +152,8 @@ hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, con
 // Four-step Welch for N = N1 * 256, 16 <= N1 <= 256: means (frames*nseg), z (frames*nseg*N)
 // workspaces; tws = W_256^m (256) ++ W_N1^m (N1).
 hipError_t launch_welch4(const float2 *x, int64_t len, const float *win, const float2 *tw,
-                         const float2 *tws, const WelchGeom &g, float2 *means, float2 *z,
-                         float *rows, int frames, hipStream_t st);
+                         const float2 *tws, const float2 *winf, const WelchGeom &g, float2 *means,
+                         float2 *z, float *rows, int frames, hipStream_t st);
 
 hipError_t launch_waterfall_init(float *ring, int H, int W, hipStream_t st);
 hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,

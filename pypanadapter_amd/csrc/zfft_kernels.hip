@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict_
                                                           const float *__restrict__ win,
                                                           const v2f *__restrict__ tw,
                                                           const v2f *__restrict__ tws, WelchGeom g,
-                                                          const v2f *__restrict__ means,
+                                                          v2f *__restrict__ means,
                                                           v2f *__restrict__ z) {
   __shared__ __attribute__((aligned(16))) v2f sh[16 * kColStride];
   const int N = g.n_fft, N1 = N / kN2, groups = N1 / 16;
@@ -1012,12 +1012,28 @@ __global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict_
   const int c = threadIdx.x & 15, t = threadIdx.x >> 4;
   const int n1 = cg * 16 + c;
   const v2f *__restrict__ seg = x + (int64_t)f * len + (int64_t)s * g.step;
-  const v2f mean = means[fs];
   v2f v[16];
+  if (g.fused_mean) {  // the mean comes off after the transform (welch4_rows_kernel)
+    v2f sum = splat(0.f);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int n = n1 + N1 * (t + 16 * i);
-    v[i] = n < g.nperseg ? (seg[n] - mean) * win[n] : splat(0.f);  // short branch: zero pad
+    for (int i = 0; i < 16; ++i) {
+      const int n = n1 + N1 * (t + 16 * i);
+      const v2f xv = seg[n];
+      sum += xv;
+      v[i] = xv * win[n];
+    }
+    __shared__ v2f red[4];
+    sum = wave_sum(sum);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) means[(int64_t)fs * groups + cg] = (red[0] + red[1]) + (red[2] + red[3]);
+  } else {
+    const v2f mean = means[fs];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = n1 + N1 * (t + 16 * i);
+      v[i] = n < g.nperseg ? (seg[n] - mean) * win[n] : splat(0.f);  // short branch: zero pad
+    }
   }
   v2f *col = sh + c * kColStride;
   stockham_pass<16>(v, t, kN2, 1, tws);
@@ -1046,9 +1062,16 @@ __global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict_
 }
 
 template <int R0>
+__device__ __forceinline__ int welch4_k1(int t, int N1, int i) {
+  return N1 == R0 ? stockham_out_index<R0>(t, N1, 1, i) : stockham_out_index<16>(t, N1, R0, i);
+}
+
+template <int R0>
 __global__ __launch_bounds__(256) void welch4_rows_kernel(const v2f *__restrict__ z,
-                                                          const v2f *__restrict__ tws, WelchGeom g,
-                                                          float *__restrict__ rows) {
+                                                          const v2f *__restrict__ tws,
+                                                          const v2f *__restrict__ winf,
+                                                          const v2f *__restrict__ means,
+                                                          WelchGeom g, float *__restrict__ rows) {
   extern __shared__ v2f shr[];
   const int N = g.n_fft, N1 = N / kN2, T16 = N1 / 16;
   const int f = blockIdx.x / (kN2 / 16), kg = blockIdx.x % (kN2 / 16);
@@ -1059,6 +1082,12 @@ __global__ __launch_bounds__(256) void welch4_rows_kernel(const v2f *__restrict_
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  v2f wf[16];  // FFT(window) at this thread's bins (fused mean)
+  if (g.fused_mean) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wf[i] = winf[k2 + kN2 * welch4_k1<R0>(t, N1, i)];
+  }
+  const int groups = N1 / 16;
   for (int s = 0; s < g.nseg; ++s) {
     const v2f *__restrict__ zr = z + ((int64_t)f * g.nseg + s) * N + (int64_t)k2 * N1;
     v2f v[16];
@@ -1073,13 +1102,21 @@ __global__ __launch_bounds__(256) void welch4_rows_kernel(const v2f *__restrict_
       stockham_pass<16>(v, t, N1, R0, tw1);
       __syncthreads();  // reads done before the next segment's store
     }
+    if (g.fused_mean) {  // X = FFT(x w) - mean FFT(w): the column groups' partial sums
+      const v2f *__restrict__ ps = means + ((int64_t)f * g.nseg + s) * groups;
+      v2f sum = splat(0.f);
+      for (int q = 0; q < groups; ++q) sum += ps[q];
+      const v2f mean = sum * (1.f / (float)g.nperseg);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] -= cmul(mean, wf[i]);
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = fmaf(v[i].x, v[i].x, fmaf(v[i].y, v[i].y, acc[i]));
   }
   float *__restrict__ row = rows + (int64_t)f * g.n_win;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int k1 = N1 == R0 ? stockham_out_index<R0>(t, N1, 1, i) : stockham_out_index<16>(t, N1, R0, i);
+    const int k1 = welch4_k1<R0>(t, N1, i);
     const int k = k2 + kN2 * k1;
     float mult;
     const int j = welch_slot(g, k, mult);
@@ -1341,28 +1378,32 @@ hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, con
 }
 
 hipError_t launch_welch4(const float2 *x, int64_t len, const float *win, const float2 *tw,
-                         const float2 *tws, const WelchGeom &g, float2 *means, float2 *z,
-                         float *rows, int frames, hipStream_t st) {
+                         const float2 *tws, const float2 *winf, const WelchGeom &g, float2 *means,
+                         float2 *z, float *rows, int frames, hipStream_t st) {
   const int N1 = g.n_fft / kN2;
   if (N1 < 16 || N1 > 256 || g.n_fft != N1 * kN2) return hipErrorInvalidValue;
+  if (g.fused_mean && !winf) return hipErrorInvalidValue;
   const unsigned segs = (unsigned)frames * (unsigned)g.nseg;
-  hipLaunchKernelGGL(welch4_means_kernel, dim3(segs), dim3(256), 0, st, (const v2f *)x, len, g,
-                     (v2f *)means);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
+  if (!g.fused_mean) {
+    hipLaunchKernelGGL(welch4_means_kernel, dim3(segs), dim3(256), 0, st, (const v2f *)x, len, g,
+                       (v2f *)means);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(welch4_cols_kernel, dim3(segs * (N1 / 16)), dim3(256), 0, st,
                      (const v2f *)x, len, win, (const v2f *)tw, (const v2f *)tws, g,
-                     (const v2f *)means, (v2f *)z);
+                     (v2f *)means, (v2f *)z);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t lds = (size_t)16 * (N1 + N1 / 16 + 2) * sizeof(v2f);
   const dim3 grid((unsigned)frames * (kN2 / 16)), block(N1);
-  const v2f *zc = (const v2f *)z, *tc = (const v2f *)tws;
+  const v2f *zc = (const v2f *)z, *tc = (const v2f *)tws, *wc = (const v2f *)winf, *mc = (const v2f *)means;
   switch (ilog2_dev(N1) % 4) {
-    case 0: hipLaunchKernelGGL(welch4_rows_kernel<16>, grid, block, lds, st, zc, tc, g, rows); break;
-    case 1: hipLaunchKernelGGL(welch4_rows_kernel<2>, grid, block, lds, st, zc, tc, g, rows); break;
-    case 2: hipLaunchKernelGGL(welch4_rows_kernel<4>, grid, block, lds, st, zc, tc, g, rows); break;
-    default: hipLaunchKernelGGL(welch4_rows_kernel<8>, grid, block, lds, st, zc, tc, g, rows); break;
+    case 0: hipLaunchKernelGGL(welch4_rows_kernel<16>, grid, block, lds, st, zc, tc, wc, mc, g, rows); break;
+    case 1: hipLaunchKernelGGL(welch4_rows_kernel<2>, grid, block, lds, st, zc, tc, wc, mc, g, rows); break;
+    case 2: hipLaunchKernelGGL(welch4_rows_kernel<4>, grid, block, lds, st, zc, tc, wc, mc, g, rows); break;
+    default: hipLaunchKernelGGL(welch4_rows_kernel<8>, grid, block, lds, st, zc, tc, wc, mc, g, rows); break;
   }
   return hipGetLastError();
 }

@@ -399,7 +399,7 @@ struct zfft_plan {
   int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows,
                 // 3 XA tiles (all-pole + FIR + half-rate all-pole)
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
-  DevBuf edge, xk, xa_tab, tws, means, z4, xa_ring;
+  DevBuf edge, xk, xa_tab, tws, means, z4, xa_ring, winf;
   int xa_fuse = 0;  // XA stages per launch (0 auto: kXaFuseAuto)
   // waterfall rendering: colormap LUT (host copy + device), levels
   uint8_t lut[256 * 4] = {};
@@ -465,6 +465,11 @@ int quiesce(zfft_plan *p);
 int use_stream(zfft_plan *p, hipStream_t st);
 int done_on(zfft_plan *p, hipStream_t st);
 
+#ifndef ZFFT_WELCH_ONEWG_MAX
+#define ZFFT_WELCH_ONEWG_MAX 16384
+#endif
+constexpr int kWelchOneWgMax = ZFFT_WELCH_ONEWG_MAX;  // auto Welch: one workgroup per frame up to here
+
 // LO table: one row of lo_len entries per LO frequency (the plan's f_lo, or the
 // zfft_plan_set_lo_frames list), rows lo_len apart.
 int ensure_lo(zfft_plan *p, int64_t L) {
@@ -493,6 +498,28 @@ int ensure_lo(zfft_plan *p, int64_t L) {
   return ZFFT_OK;
 }
 
+// In-place radix-2 DFT (forward, exp(-2 pi i k n / N)), N a power of two, float64.
+void fft64(std::vector<double> &re, std::vector<double> &im) {
+  const size_t n = re.size();
+  for (size_t i = 1, j = 0; i < n; ++i) {
+    size_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j |= bit;
+    if (i < j) std::swap(re[i], re[j]), std::swap(im[i], im[j]);
+  }
+  for (size_t len = 2; len <= n; len <<= 1) {
+    const double a = -2.0 * M_PI / (double)len;
+    for (size_t i = 0; i < n; i += len)
+      for (size_t k = 0; k < len / 2; ++k) {
+        const double c = std::cos(a * (double)k), sn = std::sin(a * (double)k);
+        const size_t u = i + k, v = u + len / 2;
+        const double tr = re[v] * c - im[v] * sn, ti = re[v] * sn + im[v] * c;
+        re[v] = re[u] - tr, im[v] = im[u] - ti;
+        re[u] += tr, im[u] += ti;
+      }
+  }
+}
+
 // welch builds get_window(window, nperseg); nperseg = min(N, L_d) (short-input branch).
 int ensure_window(zfft_plan *p, int nperseg) {
   if (p->win_len == nperseg) return ZFFT_OK;
@@ -517,6 +544,17 @@ int ensure_window(zfft_plan *p, int nperseg) {
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "window allocation failed");
   e = hipMemcpy(p->win.p, wf.data(), nperseg * sizeof(float), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "window upload");
+  if (nperseg == p->cfg.n_fft && p->cfg.n_fft >= 4096) {  // (four-step capable sizes)
+    // the four-step Welch subtracts the segment mean after its transform: X = FFT(x w) -
+    // mean FFT(w) (scipy's detrend='constant' is linear); FFT(w) of the float32 window, fp64
+    std::vector<double> re(wf.begin(), wf.end()), im(nperseg, 0.0);
+    fft64(re, im);
+    std::vector<float2> wft(nperseg);
+    for (int k = 0; k < nperseg; ++k) wft[k] = make_float2((float)re[k], (float)im[k]);
+    e = p->winf.ensure(nperseg * sizeof(float2));
+    if (e == hipSuccess) e = hipMemcpy(p->winf.p, wft.data(), nperseg * sizeof(float2), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "window transform upload");
+  }
   p->win_len = nperseg;
   p->win_ss = ss;
   return ZFFT_OK;
@@ -576,10 +614,6 @@ int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
   return ZFFT_OK;
 }
 
-#ifndef ZFFT_WELCH_ONEWG_MAX
-#define ZFFT_WELCH_ONEWG_MAX 16384
-#endif
-constexpr int kWelchOneWgMax = ZFFT_WELCH_ONEWG_MAX;  // auto Welch: one workgroup per frame up to here
 #ifndef ZFFT_WELCH4_CHUNK_MB
 #define ZFFT_WELCH4_CHUNK_MB 0  // chunks of 48/96/192 MB measured 3.1x/1.8x/1.4x slower (cfg5)
 #endif
@@ -844,13 +878,15 @@ int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, fl
     const int chunk = kWelch4ChunkBytes > 0
                           ? (int)std::max<size_t>(1, std::min<size_t>(frames, kWelch4ChunkBytes / zf))
                           : frames;
-    e = p->means.ensure((size_t)chunk * w.nseg * sizeof(float2));
+    w.fused_mean = nperseg == N ? 1 : 0;  // partial sums from the column pass (kN2-column groups)
+    e = p->means.ensure((size_t)chunk * w.nseg * (N / 256 / 16) * sizeof(float2));
     if (e == hipSuccess) e = p->z4.ensure((size_t)chunk * zf);
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "four-step Welch workspace allocation failed");
     for (int f0 = 0; f0 < frames; f0 += chunk) {
       const int nf = std::min(chunk, frames - f0);
       e = launch_welch4(x + (int64_t)f0 * Ld, Ld, p->win.as<float>(), p->tw.as<float2>(),
-                        p->tws.as<float2>(), w, p->means.as<float2>(), p->z4.as<float2>(),
+                        p->tws.as<float2>(), w.fused_mean ? p->winf.as<float2>() : nullptr, w,
+                        p->means.as<float2>(), p->z4.as<float2>(),
                         d_rows + (int64_t)f0 * p->cfg.n_win, nf, st);
       if (e != hipSuccess) return hip_fail(e, "welch4 launch");
     }
@@ -1026,7 +1062,7 @@ int zfft_plan_destroy(zfft_plan *p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->in2, &p->yf, &p->ping, &p->pong, &p->rows,
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
-                    &p->tws, &p->means, &p->z4, &p->xa_ring})
+                    &p->tws, &p->means, &p->z4, &p->xa_ring, &p->winf})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->done_ev) (void)hipEventDestroy(p->done_ev);
