@@ -70,7 +70,8 @@
 #ifndef XA_PF
 #define XA_PF 0   // next-tile load issue points: 0 = 4 groups at the tile start, 2 after the
                   // forward pass, 2 after the scan; 1 = all 8 after the forward pass;
-                  // 2 = no prefetch: a tile's loads at its own start
+                  // 2 = no prefetch: a tile's loads at its own start; 4 = all 8 at the tile
+                  // start; 5 = groups 0-3 after the flush, 4-7 at the next tile's start
 #endif
 
 namespace zfft {
@@ -602,6 +603,10 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
 #pragma unroll
       for (int g = 0; g < 8; ++g) issue_group(g);
     }
+    if (XA_PF == 5) {  // the second half of this tile's loads (the first came with the last flush)
+#pragma unroll
+      for (int g = 4; g < 8; ++g) issue_group(g);
+    }
     v2f y[B];
     {
       const bool fast = fast_tile(base);  // wave-uniform
@@ -809,7 +814,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
           issue_group(2);
           issue_group(3);
         }
-        if (XA_PF != 4) {
+        if (XA_PF != 4 && XA_PF != 5 && XA_PF != 2) {
           issue_group(4);
           issue_group(5);
         }
@@ -966,6 +971,10 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     }
     XA_STAMP(8);
     flush_tile(tau, h, ln);
+    if (XA_PF == 5) {  // half of the next tile's loads: 32 VGPRs across the tile boundary
+#pragma unroll
+      for (int g = 0; g < 4; ++g) issue_group(g);
+    }
     XA_STAMP(9);
   }
   if (XA_DEFER) issue_deferred(lane);
