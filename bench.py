@@ -59,7 +59,7 @@ CONFIGS = {
 IN_BYTES = {"complex64": 8, "complex32": 4, "cu8": 2}
 TONES = ((0.31, 1.0), (-0.57, 0.1))
 # plan launch name -> kernel-name prefix in the rocprofv3 / PMC summaries
-KERNEL_OF = {"xa_stage_mix": "xa_stage_kernel<true", "xa_stage": "xa_stage_kernel<false",
+KERNEL_OF = {"xa_stage_mix": "xa_stage_kernel<32, true", "xa_stage": "xa_stage_kernel<32, false",
              "xa_fused_mix": "xa_fused_kernel<true", "xa_fused": "xa_fused_kernel<false",
              "welch_rows": "welch_", "welch4": "welch4_"}
 

@@ -44,10 +44,25 @@ for s in $STEPS; do
     quick)
       run quick 300 python bench.py --steps 100 --warmup 3 $FAST || exit $? ;;
     cfgs)
-      run bench_cfg3 300 python bench.py --config cfg3 --steps 50 --warmup 2 $FAST || exit $?
-      run bench_cfg5 300 python bench.py --config cfg5 --steps 20 --warmup 2 $FAST || exit $?
-      run bench_cfg1 300 python bench.py --config cfg1 --steps 50 --warmup 2 $FAST || exit $?
-      run bench_cfg2_u8 300 python bench.py --in-dtype cu8 --steps 50 --warmup 2 $FAST || exit $? ;;
+      CHK="--no-cpu --no-e2e"
+      run bench_cfg3 300 python bench.py --config cfg3 --steps 50 --warmup 2 $CHK || exit $?
+      run bench_cfg5 300 python bench.py --config cfg5 --steps 20 --warmup 2 $CHK || exit $?
+      run bench_cfg5_f16 300 python bench.py --config cfg5 --in-dtype complex32 --steps 20 --warmup 2 $CHK || exit $?
+      run bench_cfg1 300 python bench.py --config cfg1 --steps 50 --warmup 2 $CHK || exit $?
+      run bench_cfg4 300 python bench.py --config cfg4 --steps 50 --warmup 2 $CHK || exit $?
+      run bench_cfg2_u8 300 python bench.py --in-dtype cu8 --steps 50 --warmup 2 $CHK || exit $?
+      run bench_cfg2_f16 300 python bench.py --in-dtype complex32 --steps 50 --warmup 2 $CHK || exit $? ;;
+    pmc5)  # cfg5 traffic, complex64 and fp16 (complex32) IQ storage
+      for dt in complex64 complex32; do
+        run pmc5_fetch_$dt 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+          -d "$OUT/pmc5_fetch_$dt" -o run -- python3 "$R/bench.py" --config cfg5 --in-dtype $dt --steps 2 --warmup 1 $FAST || exit $?
+        run pmc5_write_$dt 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+          -d "$OUT/pmc5_write_$dt" -o run -- python3 "$R/bench.py" --config cfg5 --in-dtype $dt --steps 2 --warmup 1 $FAST || exit $?
+        python3 "$R/tools/pmc_traffic.py" "$OUT/pmc5_fetch_$dt" "$OUT/pmc5_write_$dt" 2048 cfg5 \
+          "$OUT/traffic_cfg5_$dt.json" $dt > "$OUT/traffic5_$dt.log" || exit $?
+      done ;;
+    sweep)
+      run sweep 900 python tools/sweep_schedule.py "$OUT/sweep_schedule.json" || exit $? ;;
     prof)
       run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 2 $FAST || exit $? ;;

@@ -70,8 +70,8 @@ def main():
            "per_kernel": per_kernel,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
                      "bench.py; FETCH doubled per the gfx950 calibration (calibrated for 16-B-per-lane "
-                     "streaming reads; the XA stage loads are 8 B per lane, so the raw sum is "
-                     "kept as the lower bound)"}
+                     "streaming reads: the XA tile loads and the Welch loads are 16 B per lane); "
+                     "the raw sum is kept as the lower bound"}
     if out:
         json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
