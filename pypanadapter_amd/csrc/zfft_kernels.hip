@@ -975,11 +975,13 @@ static hipError_t welch_dif_launch(const float2 *x, int64_t len, const float *wi
 // the reference UI's range S:1397, N = 65536 is BASELINE cfg5).  With n = n1 + N1 n2 and
 // k = k2 + N2 k1:  X[k] = sum_n1 W_N1^(n1 k1) W_N^(n1 k2) sum_n2 x[n] W_N2^(n2 k2).
 //   welch4_means: the constant-detrend mean of every segment (one workgroup per segment)
-//   welch4_cols : 16 columns n1 per workgroup (128 B of every row n2 -> coalesced loads);
-//                 mean and window applied on load, length-256 FFT, twiddle W_N^(n1 k2),
-//                 stored as Z[k2][n1] (rows of N1 contiguous samples)
-//   welch4_rows : 16 rows k2 per workgroup, length-N1 FFT per segment, |X|^2 summed over
-//                 the segments in registers, then scale, fftshift crop and 20 log10.
+//   welch4_cols : ZFFT_W4_CPW (32) columns n1 per workgroup (256 B of every row n2 ->
+//                 coalesced loads); window applied on load (the mean's partial sums taken
+//                 beside it), length-256 FFT, twiddle W_N^(n1 k2), stored as Z[k2][n1]
+//                 (rows of N1 contiguous samples)
+//   welch4_rows : 16 rows k2 per workgroup, length-N1 FFT per segment (the next segment's
+//                 row prefetched), mean·FFT(w) subtracted, |X|^2 summed over the segments in
+//                 registers, then scale, fftshift crop and 20 log10.
 // tws = [W_256^m, m < 256] ++ [W_N1^m, m < N1].
 __global__ __launch_bounds__(256) void welch4_means_kernel(const v2f *__restrict__ x, int64_t len,
                                                            WelchGeom g, v2f *__restrict__ means) {
@@ -998,19 +1000,27 @@ __global__ __launch_bounds__(256) void welch4_means_kernel(const v2f *__restrict
 
 constexpr int kN2 = 256;
 constexpr int kColStride = 256 + 16 + 2;  // lp(256) + 2: 16 B aligned, spreads the columns
+// with 64 columns across a wave's lanes (one t) an odd column stride puts the 32 lanes of
+// each half-wave on distinct bank pairs
+template <int CPW> constexpr int col_stride() { return CPW >= 32 ? 256 + 16 + 1 : kColStride; }
 
-__global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict__ x, int64_t len,
-                                                          const float *__restrict__ win,
-                                                          const v2f *__restrict__ tw,
-                                                          const v2f *__restrict__ tws, WelchGeom g,
-                                                          v2f *__restrict__ means,
-                                                          v2f *__restrict__ z) {
-  __shared__ __attribute__((aligned(16))) v2f sh[16 * kColStride];
-  const int N = g.n_fft, N1 = N / kN2, groups = N1 / 16;
+// CPW columns per workgroup, 16 threads per column (16 * CPW threads): a wave holds 64
+// consecutive columns of one row set, so every load and store instruction moves 512
+// contiguous bytes of a row (CPW = 64; N1 < 64 uses CPW = 16)
+template <int CPW>
+__global__ __launch_bounds__(16 * CPW) void welch4_cols_kernel(const v2f *__restrict__ x, int64_t len,
+                                                               const float *__restrict__ win,
+                                                               const v2f *__restrict__ tw,
+                                                               const v2f *__restrict__ tws, WelchGeom g,
+                                                               v2f *__restrict__ means,
+                                                               v2f *__restrict__ z) {
+  extern __shared__ __attribute__((aligned(16))) v2f shc[];  // CPW columns of kColStride
+  constexpr int NT = 16 * CPW, NWV = NT / 64;
+  const int N = g.n_fft, N1 = N / kN2, groups = N1 / CPW;
   const int fs = blockIdx.x / groups, cg = blockIdx.x % groups;
   const int f = fs / g.nseg, s = fs % g.nseg;
-  const int c = threadIdx.x & 15, t = threadIdx.x >> 4;
-  const int n1 = cg * 16 + c;
+  const int c = threadIdx.x % CPW, t = threadIdx.x / CPW;
+  const int n1 = cg * CPW + c;
   const v2f *__restrict__ seg = x + (int64_t)f * len + (int64_t)s * g.step;
   v2f v[16];
   if (g.fused_mean) {  // the mean comes off after the transform (welch4_rows_kernel)
@@ -1022,11 +1032,15 @@ __global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict_
       sum += xv;
       v[i] = xv * win[n];
     }
-    __shared__ v2f red[4];
+    __shared__ v2f red[NWV];
     sum = wave_sum(sum);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
     __syncthreads();
-    if (threadIdx.x == 0) means[(int64_t)fs * groups + cg] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) {
+      v2f tot = splat(0.f);
+      for (int w = 0; w < NWV; ++w) tot += red[w];
+      means[(int64_t)fs * groups + cg] = tot;
+    }
   } else {
     const v2f mean = means[fs];
 #pragma unroll
@@ -1035,7 +1049,7 @@ __global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict_
       v[i] = n < g.nperseg ? (seg[n] - mean) * win[n] : splat(0.f);  // short branch: zero pad
     }
   }
-  v2f *col = sh + c * kColStride;
+  v2f *col = shc + c * col_stride<CPW>();
   stockham_pass<16>(v, t, kN2, 1, tws);
   stockham_store<16>(v, col, t, kN2, 1);
   __syncthreads();
@@ -1061,13 +1075,26 @@ __global__ __launch_bounds__(256) void welch4_cols_kernel(const v2f *__restrict_
   for (int i = 0; i < 16; ++i) zs[(int64_t)(t + 16 * i) * N1 + n1] = v[i];
 }
 
+// columns per workgroup of the column pass (the row pass reads that many partial sums):
+// cfg5 column pass 1.22 / 1.05 / 1.52 ms at 16 / 32 / 64 (profiles/r03_ab/r03tu)
+#ifndef ZFFT_W4_CPW
+#define ZFFT_W4_CPW 32
+#endif
+__host__ __device__ inline int welch4_cpw(int N1) { return N1 >= ZFFT_W4_CPW ? ZFFT_W4_CPW : 16; }
+
 template <int R0>
 __device__ __forceinline__ int welch4_k1(int t, int N1, int i) {
   return N1 == R0 ? stockham_out_index<R0>(t, N1, 1, i) : stockham_out_index<16>(t, N1, R0, i);
 }
 
+// Row pass at 2 waves/SIMD (216 VGPRs): capping registers for 4 or 5 waves/SIMD measured
+// 1.39 / 2.04 ms against 0.81 ms at cfg5 (profiles/r03_ab/r03tu); the next segment's
+// prefetch took it from 1.03 ms
+#ifndef ZFFT_W4_RWPE
+#define ZFFT_W4_RWPE 2
+#endif
 template <int R0>
-__global__ __launch_bounds__(256) void welch4_rows_kernel(const v2f *__restrict__ z,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZFFT_W4_RWPE))) void welch4_rows_kernel(const v2f *__restrict__ z,
                                                           const v2f *__restrict__ tws,
                                                           const v2f *__restrict__ winf,
                                                           const v2f *__restrict__ means,
@@ -1087,12 +1114,19 @@ __global__ __launch_bounds__(256) void welch4_rows_kernel(const v2f *__restrict_
 #pragma unroll
     for (int i = 0; i < 16; ++i) wf[i] = winf[k2 + kN2 * welch4_k1<R0>(t, N1, i)];
   }
-  const int groups = N1 / 16;
+  const int groups = N1 / welch4_cpw(N1);
+  const v2f *__restrict__ zr = z + (int64_t)f * g.nseg * N + (int64_t)k2 * N1 + t;
+  v2f vn[16];  // the next segment's row, loaded while this one is transformed
+#pragma unroll
+  for (int i = 0; i < 16; ++i) vn[i] = zr[i * T16];
   for (int s = 0; s < g.nseg; ++s) {
-    const v2f *__restrict__ zr = z + ((int64_t)f * g.nseg + s) * N + (int64_t)k2 * N1;
     v2f v[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = zr[t + i * T16];
+    for (int i = 0; i < 16; ++i) v[i] = vn[i];
+    if (s + 1 < g.nseg) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) vn[i] = zr[(int64_t)(s + 1) * N + i * T16];
+    }
     stockham_pass<R0>(v, t, N1, 1, tw1);
     if (N1 > R0) {
       stockham_store<R0>(v, row_sh, t, N1, 1);
@@ -1377,6 +1411,24 @@ hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, con
   }
 }
 
+template <int CPW>
+static hipError_t welch4_cols_launch(const void *x, int64_t len, const float *win, const void *tw,
+                                     const void *tws, const WelchGeom &g, void *means, void *z,
+                                     int64_t segs, int N1, hipStream_t st) {
+  const size_t lds = (size_t)CPW * col_stride<CPW>() * sizeof(v2f);
+  static bool attr = false;
+  if (!attr && lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void *)welch4_cols_kernel<CPW>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  attr = true;
+  hipLaunchKernelGGL(welch4_cols_kernel<CPW>, dim3(segs * (N1 / CPW)), dim3(16 * CPW), lds, st,
+                     (const v2f *)x, len, win, (const v2f *)tw, (const v2f *)tws, g, (v2f *)means,
+                     (v2f *)z);
+  return hipGetLastError();
+}
+
 hipError_t launch_welch4(const float2 *x, int64_t len, const float *win, const float2 *tw,
                          const float2 *tws, const float2 *winf, const WelchGeom &g, float2 *means,
                          float2 *z, float *rows, int frames, hipStream_t st) {
@@ -1391,9 +1443,14 @@ hipError_t launch_welch4(const float2 *x, int64_t len, const float *win, const f
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(welch4_cols_kernel, dim3(segs * (N1 / 16)), dim3(256), 0, st,
-                     (const v2f *)x, len, win, (const v2f *)tw, (const v2f *)tws, g,
-                     (v2f *)means, (v2f *)z);
+  const int cpw = welch4_cpw(N1);
+  if (cpw == 64)
+    e = welch4_cols_launch<64>(x, len, win, tw, tws, g, means, z, segs, N1, st);
+  else if (cpw == 32)
+    e = welch4_cols_launch<32>(x, len, win, tw, tws, g, means, z, segs, N1, st);
+  else
+    e = welch4_cols_launch<16>(x, len, win, tw, tws, g, means, z, segs, N1, st);
+  if (e != hipSuccess) return e;
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t lds = (size_t)16 * (N1 + N1 / 16 + 2) * sizeof(v2f);

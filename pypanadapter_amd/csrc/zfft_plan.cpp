@@ -879,7 +879,7 @@ int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, fl
                           ? (int)std::max<size_t>(1, std::min<size_t>(frames, kWelch4ChunkBytes / zf))
                           : frames;
     w.fused_mean = nperseg == N ? 1 : 0;  // partial sums from the column pass (kN2-column groups)
-    e = p->means.ensure((size_t)chunk * w.nseg * (N / 256 / 16) * sizeof(float2));
+    e = p->means.ensure((size_t)chunk * w.nseg * std::max(1, N / 256 / 16) * sizeof(float2));
     if (e == hipSuccess) e = p->z4.ensure((size_t)chunk * zf);
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "four-step Welch workspace allocation failed");
     for (int f0 = 0; f0 < frames; f0 += chunk) {

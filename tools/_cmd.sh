@@ -1,8 +1,9 @@
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r03r; mkdir -p $O
-for fz in 2 3; do
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/f$fz -o run -- python3 bench.py --fuse $fz --steps 2 --warmup 1 --min-seconds 0 --no-cpu --no-e2e --no-check > $O/f$fz.log 2>&1 || exit $?
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/w$fz -o run -- python3 bench.py --fuse $fz --steps 2 --warmup 1 --min-seconds 0 --no-cpu --no-e2e --no-check > $O/w$fz.log 2>&1 || exit $?
-  python3 tools/pmc_traffic.py $O/f$fz $O/w$fz 4096 cfg2 $O/traffic_cfg2_fuse$fz.json complex64 > $O/traffic_fuse$fz.log || exit $?
+O=gpurun_out/r03v; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for dt in complex64 complex32; do
+  timeout -k 10 200 python bench.py --config cfg5 --in-dtype $dt --steps 20 --warmup 2 --no-cpu --no-e2e > $O/cfg5_$dt.log 2>&1 || exit $?
+  python -c "import json; d=json.loads(open('$O/cfg5_$dt.log').read().strip().splitlines()[-1]); print('$dt', d['ms_per_step'], d['kernels'], d['parity_checked_frames'])"
 done
