@@ -93,7 +93,12 @@ struct Geo {
   static constexpr int K = B / 2;            // kept outputs per lane and tile
   static constexpr int T = 64 * B;           // tile (input samples)
   static constexpr int kRow = B + 2;         // LDS row stride (v2f): ds_read_b128 rows conflict-free
-  static constexpr int kHeldRow = K + 2;     // output-transpose rows (v2f): b128 writes conflict-free
+  // output-transpose rows (v2f): b128 writes conflict-free; the pair and single reads see
+  // 2-way conflicts on a few lanes (~30 LDS cycles per tile).  No padding makes all three
+  // conflict-free; an XOR swizzle of the 16-B slots by row does (SQ_LDS_BANK_CONFLICT
+  // 29.1 M -> 0.4 M per stage-0 dispatch) but costs 12 VALU instructions per tile for the
+  // per-slot write addresses, and measured 0.7 % slower (profiles/r03_ab/r03w)
+  static constexpr int kHeldRow = K + 2;
   static constexpr int kOutChunks = K;       // 64-output chunks per tile
   static constexpr int kRowsPerChunk = 64 / B > 0 ? 64 / B : 1;  // input rows one 64-sample chunk fills
   // LDS per wave: the tile transpose (both halves) + FIR carry (12 used) + frame-end v
@@ -370,8 +375,12 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   constexpr int K = G::K, T = G::T, kRow = G::kRow, kHeldRow = G::kHeldRow, kChunks = G::kOutChunks;
   __shared__ __attribute__((aligned(16))) v2f lds_all[kWaves][G::kBuf];
   const CT tab = (CT)tab_g;
-  __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];  // lag rows, copied once
-  for (int i = threadIdx.x; i < kXaLag * 2; i += 64 * kWaves) lag_l[i] = ((const v4f *)tab_g->lag)[i];
+  // lag rows, copied once as two planes (the rows' first and second 16 B): a lane per row
+  // d reads 16 B at a 16-B stride, conflict-free per ds_read_b128 group (rows of 32 B, read
+  // whole, put 16 lanes on 8 bank slots: 2-way)
+  __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];
+  for (int i = threadIdx.x; i < kXaLag * 2; i += 64 * kWaves)
+    lag_l[(i & 1) * kXaLag + (i >> 1)] = ((const v4f *)tab_g->lag)[i];
   __shared__ v4f xw_l[2][16];  // cross-row scan weights (XaPass::xr), forward / backward
   if (threadIdx.x < 32) xw_l[threadIdx.x >> 4][threadIdx.x & 15] = ((const v4f *)((threadIdx.x >> 4) ? tab_g->b.xr : tab_g->f.xr))[threadIdx.x & 15];
   __syncthreads();
@@ -964,8 +973,8 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
 #pragma unroll
       for (int c = 0; c < kLagChunks; ++c) {
         const int d = kXaLag - 1 - 64 * c - ln;
-        lg[2 * c] = lag_l[2 * d];
-        lg[2 * c + 1] = lag_l[2 * d + 1];
+        lg[2 * c] = lag_l[d];
+        lg[2 * c + 1] = lag_l[kXaLag + d];
       }
       finish_held(tau - 1, &q_exit, lg, ln);
     }
@@ -1021,13 +1030,14 @@ __global__ __launch_bounds__(64 * kWaves, 2) void xa_fused_kernel(
   using G = Geo<B>;
   constexpr int K = G::K, T = G::T, kRow = G::kRow, kHeldRow = G::kHeldRow, kChunks = G::kOutChunks;
   constexpr int kRowH = B / 2 + 2;              // column-half transpose rows (144 B)
-  constexpr int kMainF = 64 * kHeldRow;         // = 64 kRowH: either transpose
+  constexpr int kMainF = 64 * (B / 2 + 2);      // = 64 kRowH: either transpose
   static_assert(64 * kRowH == kMainF && 4 * kRow <= kMainF, "LDS geometry");
   __shared__ __attribute__((aligned(16))) v2f lds_all[kWaves][kMainF];
   __shared__ __attribute__((aligned(16))) StageLds sl_all[kWaves][3];
   const CT tab = (CT)tab_g;
-  __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];
-  for (int i = threadIdx.x; i < kXaLag * 2; i += 64 * kWaves) lag_l[i] = ((const v4f *)tab_g->lag)[i];
+  __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];  // two planes, as above
+  for (int i = threadIdx.x; i < kXaLag * 2; i += 64 * kWaves)
+    lag_l[(i & 1) * kXaLag + (i >> 1)] = ((const v4f *)tab_g->lag)[i];
   __shared__ v4f xw_l[2][16];
   if (threadIdx.x < 32) xw_l[threadIdx.x >> 4][threadIdx.x & 15] = ((const v4f *)((threadIdx.x >> 4) ? tab_g->b.xr : tab_g->f.xr))[threadIdx.x & 15];
   __syncthreads();
@@ -1404,7 +1414,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void xa_fused_kernel(
         v2f v = ((LP)sl->held[c])[ln];
         if (q != nullptr) {
           const int d = kXaLag - 1 - 64 * c - ln;
-          const v4f l0 = lag_l[2 * d], l1 = lag_l[2 * d + 1];
+          const v4f l0 = lag_l[d], l1 = lag_l[kXaLag + d];
           v = vfma(splat(l0.x), q->r[0], v);
           v = vfma(splat(l0.y), q->r[1], v);
           v = vfma(splat(l0.z), q->r[2], v);
