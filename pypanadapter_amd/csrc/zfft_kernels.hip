@@ -1093,26 +1093,33 @@ __device__ __forceinline__ int welch4_k1(int t, int N1, int i) {
 #ifndef ZFFT_W4_RWPE
 #define ZFFT_W4_RWPE 2
 #endif
-template <int R0>
+// PRUNE (two-sided rows with n_win <= N/8, every zoom >= 8; N1 > R0): the crop keeps bins
+// |k| < N/16, i.e. only the last radix-16 pass's outputs 0 and 15 (k1 = t + Ns r, r = 0, 15:
+// the top digit is resolved last), so that pass forms just those two sums and the thread
+// keeps 2 accumulators and 2 FFT(window) values instead of 16 (the FFT(window) gathers were
+// half the pass's time at cfg5)
+template <int R0, bool PRUNE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZFFT_W4_RWPE))) void welch4_rows_kernel(const v2f *__restrict__ z,
                                                           const v2f *__restrict__ tws,
                                                           const v2f *__restrict__ winf,
                                                           const v2f *__restrict__ means,
                                                           WelchGeom g, float *__restrict__ rows) {
   extern __shared__ v2f shr[];
+  constexpr int NO = PRUNE ? 2 : 16;  // outputs kept per thread: i = 0, 15 when pruned
+  auto out_i = [](int o) { return PRUNE ? 15 * o : o; };
   const int N = g.n_fft, N1 = N / kN2, T16 = N1 / 16;
   const int f = blockIdx.x / (kN2 / 16), kg = blockIdx.x % (kN2 / 16);
   const int c = threadIdx.x / T16, t = threadIdx.x % T16;
   const int k2 = kg * 16 + c;
   const v2f *__restrict__ tw1 = tws + kN2;
   v2f *row_sh = shr + c * (lp(N1) + 2);
-  float acc[16];
+  float acc[NO];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  v2f wf[16];  // FFT(window) at this thread's bins (fused mean)
+  for (int i = 0; i < NO; ++i) acc[i] = 0.f;
+  v2f wf[NO];  // FFT(window) at this thread's bins (fused mean)
   if (g.fused_mean) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) wf[i] = winf[k2 + kN2 * welch4_k1<R0>(t, N1, i)];
+    for (int i = 0; i < NO; ++i) wf[i] = winf[k2 + kN2 * welch4_k1<R0>(t, N1, out_i(i))];
   }
   const int groups = N1 / welch4_cpw(N1);
   const v2f *__restrict__ zr = z + (int64_t)f * g.nseg * N + (int64_t)k2 * N1 + t;
@@ -1133,7 +1140,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZFFT_W4_RWP
       __syncthreads();
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = row_sh[lp(t + r * T16)];
-      stockham_pass<16>(v, t, N1, R0, tw1);
+      if constexpr (PRUNE) {  // the last pass's twiddles (stockham_pass<16>, Ns = R0), then
+                              // X_0 = sum v_m and X_15 = sum v_m W16^(-m)
+        const int ts = (t & (R0 - 1)) * (N1 / (16 * R0));
+        const v2f bp[4] = {tw1[ts], tw1[2 * ts], tw1[4 * ts], tw1[8 * ts]};
+        apply_powers(v, bp);
+        v2f a0 = v[0], a1 = v[0];
+#pragma unroll
+        for (int m = 1; m < 16; ++m) {
+          a0 += v[m];
+          a1 += cmul2(v[m], w16(16 - m));
+        }
+        v[0] = a0;
+        v[1] = a1;
+      } else {
+        stockham_pass<16>(v, t, N1, R0, tw1);
+      }
       __syncthreads();  // reads done before the next segment's store
     }
     if (g.fused_mean) {  // X = FFT(x w) - mean FFT(w): the column groups' partial sums
@@ -1142,15 +1164,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZFFT_W4_RWP
       for (int q = 0; q < groups; ++q) sum += ps[q];
       const v2f mean = sum * (1.f / (float)g.nperseg);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] -= cmul(mean, wf[i]);
+      for (int i = 0; i < NO; ++i) v[i] -= cmul(mean, wf[i]);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = fmaf(v[i].x, v[i].x, fmaf(v[i].y, v[i].y, acc[i]));
+    for (int i = 0; i < NO; ++i) acc[i] = fmaf(v[i].x, v[i].x, fmaf(v[i].y, v[i].y, acc[i]));
   }
   float *__restrict__ row = rows + (int64_t)f * g.n_win;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k1 = welch4_k1<R0>(t, N1, i);
+  for (int i = 0; i < NO; ++i) {
+    const int k1 = welch4_k1<R0>(t, N1, out_i(i));
     const int k = k2 + kN2 * k1;
     float mult;
     const int j = welch_slot(g, k, mult);
@@ -1456,12 +1478,24 @@ hipError_t launch_welch4(const float2 *x, int64_t len, const float *win, const f
   const size_t lds = (size_t)16 * (N1 + N1 / 16 + 2) * sizeof(v2f);
   const dim3 grid((unsigned)frames * (kN2 / 16)), block(N1);
   const v2f *zc = (const v2f *)z, *tc = (const v2f *)tws, *wc = (const v2f *)winf, *mc = (const v2f *)means;
+#ifndef ZFFT_W4_PRUNE
+#define ZFFT_W4_PRUNE 1
+#endif
+  const bool prune = ZFFT_W4_PRUNE && !g.onesided && N1 > 16 && (int64_t)g.n_win * 8 <= g.n_fft;
+#define W4_ROWS(R)                                                                                    \
+  do {                                                                                                \
+    if (prune)                                                                                        \
+      hipLaunchKernelGGL((welch4_rows_kernel<R, true>), grid, block, lds, st, zc, tc, wc, mc, g, rows);  \
+    else                                                                                              \
+      hipLaunchKernelGGL((welch4_rows_kernel<R, false>), grid, block, lds, st, zc, tc, wc, mc, g, rows); \
+  } while (0)
   switch (ilog2_dev(N1) % 4) {
-    case 0: hipLaunchKernelGGL(welch4_rows_kernel<16>, grid, block, lds, st, zc, tc, wc, mc, g, rows); break;
-    case 1: hipLaunchKernelGGL(welch4_rows_kernel<2>, grid, block, lds, st, zc, tc, wc, mc, g, rows); break;
-    case 2: hipLaunchKernelGGL(welch4_rows_kernel<4>, grid, block, lds, st, zc, tc, wc, mc, g, rows); break;
-    default: hipLaunchKernelGGL(welch4_rows_kernel<8>, grid, block, lds, st, zc, tc, wc, mc, g, rows); break;
+    case 0: W4_ROWS(16); break;
+    case 1: W4_ROWS(2); break;
+    case 2: W4_ROWS(4); break;
+    default: W4_ROWS(8); break;
   }
+#undef W4_ROWS
   return hipGetLastError();
 }
 
