@@ -2,7 +2,8 @@
 # One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel-trace / PMC summaries.
 # Every GPU step has its own time limit; a crash/abort/timeout (anything but a plain test
 # failure) ends the session so nothing else touches a possibly faulted GPU.
-# usage: tools/gpu_session.sh <tag> [steps...]   steps: tests smoke bench quick prof pmc sq cfgs
+# usage: tools/gpu_session.sh <tag> [steps...]   steps: tests smoke bench driver quick prof pmc sq
+#        stamp cfgs pmc5 sweep
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 2
@@ -78,8 +79,10 @@ for s in $STEPS; do
         SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT \
         GRBM_GUI_ACTIVE --output-format csv \
         -d "$OUT/pmc_sq" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 $FAST || exit $?
-      python3 "$R/tools/sq_counters.py" "$OUT/pmc_sq" 4096 cfg2 complex64 "$OUT/sq_cfg2.json" \
+      python3 "$R/tools/sq_counters.py" "$OUT/pmc_sq" 4096 cfg2 complex64 "$OUT/sq_cfg2.json" 299008 \
         > "$OUT/sq.log" || exit $? ;;
+    stamp)  # this session's PMC/SQ summaries become the ones bench.py reads (same sources)
+      cp "$OUT/traffic_cfg2.json" "$OUT/sq_cfg2.json" "$R/profiles/" || exit $? ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac

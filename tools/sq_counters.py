@@ -13,8 +13,11 @@ the per-instruction table).  Derived per dispatch:
   wave_valu      = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: one wave's VALU issue share
   wave_wait      = SQ_WAIT_ANY / SQ_WAVE_CYCLES (parked on s_waitcnt / barrier),
   wave_stall     = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (issue stalls)
+  valu_per_tile  = SQ_INSTS_VALU / (frames * samples / 2048) for the stage-0 kernel (its input
+                   is the frame: `samples` per frame, 2048-sample tiles; SQ_INSTS_VALU counts
+                   wave instructions)
 
-usage: sq_counters.py <dir> [frames config in_dtype out.json]
+usage: sq_counters.py <dir> [frames config in_dtype out.json [samples_per_frame]]
 """
 import csv
 import glob
@@ -70,11 +73,16 @@ def main():
            "method": __doc__.split("usage:")[0].strip()}
     if len(sys.argv) > 4:
         res.update(frames=int(sys.argv[2]), config=sys.argv[3], in_dtype=sys.argv[4])
+    if len(sys.argv) > 6:
+        frames, samples = int(sys.argv[2]), int(sys.argv[6])
+        for k, v in per.items():
+            if k.startswith("xa_stage_kernel<32, true") and "SQ_INSTS_VALU" in v:
+                v["valu_per_tile"] = round(v["SQ_INSTS_VALU"] / (frames * samples / 2048), 1)
     if len(sys.argv) > 5:
         json.dump(res, open(sys.argv[5], "w"), indent=1)
     for k, v in per.items():
         print(k, {c: v[c] for c in ("valu_busy", "waves_per_simd", "wave_valu", "wave_wait",
-                                    "wave_stall") if c in v})
+                                    "wave_stall", "valu_per_tile") if c in v})
 
 
 if __name__ == "__main__":
