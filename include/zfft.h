@@ -215,15 +215,17 @@ int zfft_plan_path(zfft_plan *plan, int32_t path);
  * holds n rows of n_samples complex64 (n <= 256).  Waits for the plan's enqueued work. */
 int zfft_plan_set_lo_frames(zfft_plan *plan, const double *f_lo, int32_t n, int32_t frames_per_lo);
 
-/* XA schedule (path 3): decimation stages per launch.  0 = automatic (3), 1 = one launch
+/* XA schedule (path 3): decimation stages per launch.  0 = automatic (1), 1 = one launch
  * per stage (stage outputs round-trip through device memory), 2 or 3 = that many
  * consecutive stages in one launch, handing over through per-frame rings of 4096 samples
- * (32 KB per frame and fused pair, cache-resident).  Same rows; diagnostics / A-B only. */
+ * (32 KB per frame and fused pair; at full batches the rings outgrow L2 and the fused
+ * launch is slower).  Same rows within the XA tolerance; diagnostics / A-B. */
 int zfft_plan_fuse(zfft_plan *plan, int32_t stages);
 
-/* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 8192, four-step
+/* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 16384, four-step
  * beyond), 1 = one workgroup per frame (n_fft <= 16384), 2 = four-step N1 x 256 (n_fft in
- * [4096, 65536]).  Same rows within the parity gate; diagnostics / A-B only. */
+ * [4096, 65536]; its row pass forms only the bins the crop keeps when n_win <= n_fft / 8).
+ * Same rows within the parity gate; diagnostics / A-B only. */
 int zfft_plan_welch(zfft_plan *plan, int32_t mode);
 
 const char *zfft_last_error(void);

@@ -199,6 +199,23 @@ def test_welch_one_workgroup_forms_vs_oracle(oracle_lib, N, z, W, F):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, z, W), f"N={N} W={W} frame {f}")
 
 
+@pytest.mark.parametrize("N,z,W", [(32768, 8, 4096), (32768, 8, 4100), (65536, 16, 4096),
+                                   (65536, 8, 8200), (16384, 8, 2048), (8192, 8, 1024),
+                                   (4096, 8, 512), (16384, 4, 4096)])
+def test_four_step_pruned_row_pass_vs_oracle(oracle_lib, N, z, W):
+    """Four-step Welch (mode 2): the row pass keeps only the last radix-16 pass's outputs 0
+    and 15 when the crop keeps |k| < N/16 (W <= N/8, N1 > 16); at W just above N/8 and at
+    N1 = 16 it runs the full pass.  Both against the float64 oracle."""
+    from pypanadapter_amd import ZoomFFT
+    L = N * z * 3
+    x = _frames(2, L, N, z, W, seed0=7100 + N // 1024 + z)
+    with ZoomFFT(N, z, 2.4e6, n_win=W) as plan:
+        plan.set_welch(2)
+        rows = plan.rows(x)
+    for f in range(2):
+        assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, z, W), f"N={N} z={z} W={W} frame {f}")
+
+
 @pytest.mark.parametrize("block,warm", [(512, 192), (1024, 256), (64, 192), (8192, 128)])
 def test_block_and_warmup_invariance(oracle_lib, block, warm):
     """The result must not depend on how frames are cut into lanes (within the gate)."""
