@@ -735,6 +735,12 @@ __global__ __launch_bounds__(MAXT, 1) void welch_rows_kernel(const v2f *__restri
 // PRUNE (W <= 2N/RL): the fftshift crop keeps only last-stage outputs 0 and RL-1, so the
 // last stage forms just those two per block.
 // Register plans (measured on MI355X):
+#ifndef ZFFT_DIF_BUF
+#define ZFFT_DIF_BUF 1  // segment and window loads through buffer resources (0: global loads)
+#endif
+#ifndef ZFFT_DIF_PP
+#define ZFFT_DIF_PP 1   // two prefetch arrays used in turn, N < 16384 (0: one, copied into v
+#endif                  // each segment): cfg2 Welch 0.486 -> 0.46 ms (profiles/r03_ab/r03dpp)
 constexpr int kDifPf = 16;             // values per thread prefetched a segment ahead (N = 4096)
 constexpr int kDifPfSmall = 8;         // the same for N <= 2048
 constexpr int kDifWaves = 3;           // waves per SIMD the registers are cut for (PRUNE, N = 4096)
@@ -796,7 +802,9 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
   const int f = min(blk * D::FPB + fl, frames - 1);
   const bool owner = blk * D::FPB + fl < frames;
   v2f *img = dyn_sh + fl * D::SLOTS;
+#if !ZFFT_DIF_BUF
   const v2f *__restrict__ xf = x + (int64_t)f * len;
+#endif
   auto sync = [&]() {
     if constexpr (D::NW > 1) __syncthreads();
     else __builtin_amdgcn_wave_barrier();
@@ -816,32 +824,56 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
       b2[i] = D::PM >= 2 ? base_of(2, t, i) : splat(0.f);
     }
   }
+#if ZFFT_DIF_BUF
+  // segment loads through a buffer resource per segment (a wave holds one frame, T >= 64:
+  // the frame base is wave-uniform): the lane offset t*8 is one VGPR for the whole kernel and
+  // the per-value offset T*r*8 an immediate or SGPR -- no 64-bit address arithmetic per load
+  const v2f *xw = x + (int64_t)__builtin_amdgcn_readfirstlane(f) * len;
+  auto seg_rsrc = [&](int s) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(xw + (int64_t)s * g.step), (short)0, N * 8, 0x00020000);
+  };
+  auto ldx = [&](__amdgpu_buffer_rsrc_t rs, int tt, int r) -> v2f {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)(tt * 8), (uint32_t)(T * r * 8), 0);
+    v2f v;
+    __builtin_memcpy(&v, &u, 8);
+    return v;
+  };
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void *)win, (short)0, N * 4, 0x00020000);
+  auto ldw = [&](int tt, int r) -> float {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wrs, (uint32_t)(tt * 4), (uint32_t)(T * r * 4), 0));
+  };
+#define DIF_X(s, tt, r) ldx(seg_rsrc(s), tt, r)
+#define DIF_W(tt, r) ldw(tt, r)
+#else
+#define DIF_X(s, tt, r) xf[(int64_t)(s) * g.step + (tt) + T * (r)]
+#define DIF_W(tt, r) win[(tt) + T * (r)]
+#endif
   auto load_seg = [&](v2f *dst, int s, int t) {
-    const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
 #pragma unroll
-    for (int r = 0; r < PF; ++r) dst[r] = seg[t + T * r];
+    for (int r = 0; r < PF; ++r) dst[r] = DIF_X(s, t, r);
   };
   // partial sums of segment s: the prefetched values plus the rest read again
   auto post_sum = [&](const v2f *v, int slot, int s, int t) {
     v2f sum = splat(0.f);
 #pragma unroll
     for (int r = 0; r < PF; ++r) sum += v[r];
-    const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
 #pragma unroll
-    for (int r = PF; r < 16; ++r) sum += seg[t + T * r];
+    for (int r = PF; r < 16; ++r) sum += DIF_X(s, t, r);
     sum = wave_sum(sum);
     if ((t & 63) == 0) red[fl][slot][t >> 6] = sum;
   };
-  v2f pf[PF > 0 ? PF : 1];
-  load_seg(pf, 0, threadIdx.x % T);
-  post_sum(pf, 0, 0, threadIdx.x % T);
+  constexpr int PFN = PF > 0 ? PF : 1;
+  v2f pfa[PFN], pfb[PFN];  // ping-pong prefetch: segment s's values arrive in one, s+1's in
+                           // the other (a single array was copied into v every segment)
+  load_seg(pfa, 0, threadIdx.x % T);
+  post_sum(pfa, 0, 0, threadIdx.x % T);
   sync();
   constexpr int NACC = PRUNE ? 2 * (16 / D::RL) : 16;
   float acc[NACC];
 #pragma unroll
   for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
 
-  for (int s = 0; s < g.nseg; ++s) {
+  auto seg_step = [&](const int s, v2f (&pf)[PFN], v2f (&pn)[PFN]) {
     // opaque per-segment copies: twiddle powers and LDS addresses are rebuilt in the loop
     // rather than hoisted out of it (dozens of registers held across the loop)
     int t = D::FPB == 1 ? (int)threadIdx.x : (int)threadIdx.x % T;
@@ -853,9 +885,8 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
     }
     v2f v[16];
     {  // values [0, PF) were prefetched a segment ahead, the rest load now
-      const v2f *__restrict__ seg = xf + (int64_t)s * g.step;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = r < PF ? pf[r] : seg[t + T * r];
+      for (int r = 0; r < 16; ++r) v[r] = r < PF ? pf[r] : DIF_X(s, t, r);
     }
     const bool more = s + 1 < g.nseg;
     // (addresses from the loop-invariant thread id: computed once, outside the loop)
@@ -863,12 +894,11 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
       if (2 * g.step == N) {
         // 50 % overlap (scipy's default noverlap): segment s+1's values [0, 8) are this
         // segment's raw [8, 16) -- only [8, PF) are loaded
-        const v2f *__restrict__ nseg = xf + (int64_t)(s + 1) * g.step;
         const int tt = (int)threadIdx.x % T;
 #pragma unroll
-        for (int r = 0; r < PF; ++r) pf[r] = r < 8 ? v[r + 8] : nseg[tt + T * r];
+        for (int r = 0; r < PF; ++r) pn[r] = r < 8 ? v[r + 8] : DIF_X(s + 1, tt, r);
       } else {
-        load_seg(pf, s + 1, (int)threadIdx.x % T);
+        load_seg(pn, s + 1, (int)threadIdx.x % T);
       }
     }
     {
@@ -877,7 +907,7 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
       for (int w = 0; w < D::NW; ++w) sum += red[fl][s & 1][w];
       const v2f mean = sum * (1.f / (float)N);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = (v[r] - mean) * win[t + T * r];
+      for (int r = 0; r < 16; ++r) v[r] = (v[r] - mean) * DIF_W(t, r);
     }
     // stage 1: DFT16 over the thread's own samples, twiddle, store at t + T k
     dft<16>(v);
@@ -903,11 +933,11 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
       }
 #pragma unroll
       for (int k = 0; k < 16; ++k) img[dif_slot(base + S16 * k)] = v[k];
-      if (st == D::PM && more) post_sum(pf, (s + 1) & 1, s + 1, t);  // next mean, read after 2 syncs
+      if (st == D::PM && more) post_sum(pn, (s + 1) & 1, s + 1, t);  // next mean, read after 2 syncs
       sync();
     }
     if (D::PM < 2 && more) {  // (no middle stage: post before the last barrier instead)
-      post_sum(pf, (s + 1) & 1, s + 1, t);
+      post_sum(pn, (s + 1) & 1, s + 1, t);
       sync();
     }
     // last stage: the thread's 16 consecutive slots as 16/RL blocks of RL
@@ -933,6 +963,15 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
       }
     }
     sync();  // last-stage reads done before the next segment's stage-1 stores
+    };
+  if constexpr (ZFFT_DIF_PP && N != 16384) {  // N = 16384 (4-value prefetch): one array
+    for (int s = 0; s < g.nseg; s += 2) {      // measured faster (0.69 vs 0.78 ms at cfg3)
+      seg_step(s, pfa, pfb);
+      if (s + 1 < g.nseg) seg_step(s + 1, pfb, pfa);
+    }
+  } else {
+    (void)pfb;
+    for (int s = 0; s < g.nseg; ++s) seg_step(s, pfa, pfa);
   }
   const int t = threadIdx.x % T;
   float *__restrict__ row = rows + (int64_t)f * g.n_win;
@@ -946,6 +985,9 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
     if (j >= 0) row[j] = 20.f * log10f(acc[i] * g.scale * mult);
   }
 }
+
+#undef DIF_X
+#undef DIF_W
 
 template <int N>
 static hipError_t welch_dif_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
