@@ -1,0 +1,399 @@
+// pc_kernels.hip -- "PC" (polyphase cascade) decimator for zoom 8 on gfx950 (tables:
+// pc_tables.cpp; design model: tools/pc_model.py).
+//
+// Three x scipy.signal.decimate(x, 2) (pypanadapter_spectrum.py:2096-2098) as, exactly,
+//   K1  y1 = (g0 * x)|2,  y2 = (g1 * y1)|2          two FIRs (33, 49 taps): no recurrence at the
+//                                                   input rate, independent tiles
+//   K2  z2 = S(v) S(1/v) y2                         two sections at rate 1/4 (zero phase)
+//       u3 = (g2 * z2)|2                            FIR (57 taps)
+//       out = A(w) A(1/w) u3                        10 sections at the output rate
+//   K3  out += U (V^T x_edge)                       frame-start / frame-end maps (rank ~10)
+// on the frame extended by zeros.  Recurrences run over lane blocks: every lane runs its
+// block from a zero state, the exit states are combined by a Kogge-Stone scan over lanes
+// (depth from the block decay, pc_own_levels / pc_ap_levels), and each output gets the
+// entering state's response ct[t] . s (t < its decay length).  K2 tiles carry warm-up halos
+// (own rate 330 samples, output rate 80) instead of state across tiles, so every tile and
+// every K1 tile is independent.
+// Intermediates: only y2 (rate 1/4, 8 B per 4 input samples) goes through device memory.
+#include "zfft_device.h"
+
+namespace zfft {
+namespace pc {
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef v2f __attribute__((address_space(3))) *LP;
+typedef v4f __attribute__((address_space(3))) *LP4;
+typedef const PcTab __attribute__((address_space(4))) *CT;
+typedef const PcSec __attribute__((address_space(4))) &CS;
+
+__device__ __forceinline__ v2f shup(v2f v, int d) {
+  return v2f{__shfl_up(v.x, d, 64), __shfl_up(v.y, d, 64)};
+}
+__device__ __forceinline__ v2f shdn(v2f v, int d) {
+  return v2f{__shfl_down(v.x, d, 64), __shfl_down(v.y, d, 64)};
+}
+__device__ __forceinline__ v2f shxor(v2f v, int d) {
+  return v2f{__shfl_xor(v.x, d, 64), __shfl_xor(v.y, d, 64)};
+}
+// An opaque copy of the table pointer per phase: the scalar loads of a phase's coefficients
+// are not hoisted out of it (hoisted, all 12 sections' tables would sit in SGPRs and spill).
+__device__ __forceinline__ CT fresh(CT p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ v2f lo2(v4f w) { return v2f{w.x, w.y}; }
+__device__ __forceinline__ v2f hi2(v4f w) { return v2f{w.z, w.w}; }
+__device__ __forceinline__ v4f cat(v2f a, v2f b) { return v4f{a.x, a.y, b.x, b.y}; }
+
+// ---------------------------------------------------------------------------------- K1
+
+constexpr int kXRow = 18;  // input tile: rows of 16 samples padded to 18 (b128 reads conflict-free)
+constexpr int kYRow = 10;  // y1: rows of 8 padded to 10
+constexpr int kXRows = kPcK1In / 16;
+__device__ __forceinline__ int xidx(int s) { return (s >> 4) * kXRow + (s & 15); }
+
+// x[n], x[n+1] of frame f (both inside the frame), as complex64
+template <int DT, int FLIP>
+__device__ __forceinline__ void load_pair(const InDesc &in, int64_t f, int64_t n, v2f &a, v2f &b) {
+  const int64_t k = f * in.stride + (FLIP ? in.len - 2 - n : n);  // first raw element
+  v2f p, q;
+  if constexpr (DT == kInC64) {
+    const v4f w = *(const v4f *)((const v2f *)in.p + k);
+    p = lo2(w);
+    q = hi2(w);
+  } else if constexpr (DT == kInC32H) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const h4 w = *(const h4 *)((const h2 *)in.p + k);
+    p = v2f{(float)w.x, (float)w.y};
+    q = v2f{(float)w.z, (float)w.w};
+  } else if constexpr (DT == kInF32R) {
+    const float2 w = *(const float2 *)((const float *)in.p + k);
+    p = v2f{w.x, 0.f};
+    q = v2f{w.y, 0.f};
+  } else {
+    typedef unsigned char u8x4 __attribute__((ext_vector_type(4)));
+    const u8x4 w = *(const u8x4 *)((const u8x2 *)in.p + k);
+    const float s = 1.f / 127.5f;
+    p = v2f{((float)w.x - 127.5f) * s, ((float)w.y - 127.5f) * s};
+    q = v2f{((float)w.z - 127.5f) * s, ((float)w.w - 127.5f) * s};
+  }
+  a = FLIP ? q : p;
+  b = FLIP ? p : q;
+}
+
+// One tile: y2 for q in [q_s, q_s + 992), q_s = -16 + 992 tile, from the mixed input
+// x[4 q_s - 64, + 4128) (zero outside the frame):
+//   y1[m] = sum_t g0[t + 16] x[2m - t],  m in [2 q_s - 24, + 2048)   (8 per thread)
+//   y2[q] = sum_t g1[t + 24] y1[2q - t]                            (4 per thread)
+template <int DT, int FLIP>
+__global__ void __launch_bounds__(256) pc_fir_kernel(InDesc in, const v2f *lo, v2f *y2,
+                                                     int64_t y2s, CT tab) {
+  __shared__ v4f lds4[kXRows * kXRow / 2];
+  const LP xl = (LP)lds4;
+  const int t = threadIdx.x;
+  const int tile = blockIdx.x;
+  const int64_t f = blockIdx.y, L = in.len;
+  const int64_t xs = 4 * ((int64_t)kPcQ0 + (int64_t)kPcK1Q * tile) - 64;
+  const v2f *lor = lo_row(lo, in, f);
+  if (xs >= 0 && xs + kPcK1In <= L) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int s = 2 * t + 512 * i;
+      if (i == 8 && t >= (kPcK1In - 4096) / 2) break;
+      v2f a, b;
+      load_pair<DT, FLIP>(in, f, xs + s, a, b);
+      const v4f l = *(const v4f *)(lor + xs + s);
+      *(LP4)(xl + xidx(s)) = cat(cmul2(a, lo2(l)), cmul2(b, hi2(l)));
+    }
+  } else {
+    for (int s = t; s < kPcK1In; s += 256) {
+      const int64_t n = xs + s;
+      v2f v = splat(0.f);
+      if (n >= 0 && n < L) v = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
+      xl[xidx(s)] = v;
+    }
+  }
+  __syncthreads();
+  v2f acc[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) acc[r] = splat(0.f);
+  {
+    const LP xb = xl + t * kXRow;  // local sample 16 t; outputs i = 8t + r read [16t + 2r, + 32]
+#pragma unroll
+    for (int p = 0; p < 24; ++p) {
+      const int j = 2 * p;
+      const v4f w = *(LP4)(xb + (j >> 4) * kXRow + (j & 15));
+      const v2f x0 = lo2(w), x1 = hi2(w);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int u = j - 2 * r;
+        if (u >= 0 && u < kPcG0) acc[r] = vfma(splat(tab->g0[u]), x0, acc[r]);
+        if (u + 1 >= 0 && u + 1 < kPcG0) acc[r] = vfma(splat(tab->g0[u + 1]), x1, acc[r]);
+      }
+    }
+  }
+  __syncthreads();
+  const LP yl = xl;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) *(LP4)(yl + t * kYRow + 2 * q) = cat(acc[2 * q], acc[2 * q + 1]);
+  __syncthreads();
+  if (t < kPcK1Q / 4) {
+    v2f b[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b[r] = splat(0.f);
+    const LP yb = yl + t * kYRow;  // y1 local 8t; outputs k = 4t + r read [2k, 2k + 48]
+#pragma unroll
+    for (int p = 0; p < 28; ++p) {
+      const int j = 2 * p;
+      const v4f w = *(LP4)(yb + (j >> 3) * kYRow + (j & 7));
+      const v2f x0 = lo2(w), x1 = hi2(w);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int u = j - 2 * r;
+        if (u >= 0 && u < kPcG1) b[r] = vfma(splat(tab->g1[u]), x0, b[r]);
+        if (u + 1 >= 0 && u + 1 < kPcG1) b[r] = vfma(splat(tab->g1[u + 1]), x1, b[r]);
+      }
+    }
+    v2f *o = y2 + f * y2s + (int64_t)kPcK1Q * tile + 4 * t;
+    *(v4f *)o = cat(b[0], b[1]);
+    *(v4f *)(o + 2) = cat(b[2], b[3]);
+  }
+}
+
+// ---------------------------------------------------------------------------------- K2
+
+// One all-pole section over this lane's block v[0..B) in time order (UP) or reversed (!UP),
+// the neighbouring lane blocks of the wave adjacent in time; XW: the 4 waves of the block
+// continue each other (cross-wave step through scr, which holds 4 waves x 2 states).
+template <int B, int LEV, int DCUT, bool UP, bool XW, bool OWN, int SI>
+__device__ __forceinline__ void sec_block(v2f (&v)[B], CT tab0, LP scr, int lane, int wave) {
+  const CT tab = fresh(tab0);
+  CS S = OWN ? tab->own[SI] : tab->ap[SI];
+  const float __attribute__((address_space(4))) *xw = &tab->own_x[OWN ? SI : 0][0][0];
+  const v2f na1 = splat(-S.a1), na2 = splat(-S.a2);
+  v2f y1 = splat(0.f), y2 = splat(0.f);
+#pragma unroll
+  for (int c = 0; c < B; ++c) {
+    const int k = UP ? c : B - 1 - c;
+    const v2f y = vfma(na1, y1, vfma(na2, y2, v[k]));
+    y2 = y1;
+    y1 = y;
+    v[k] = y;
+  }
+  v2f e0 = y1, e1 = y2;  // exit state from a zero entering state
+#pragma unroll
+  for (int d = 0; d < LEV; ++d) {
+    const int sh = 1 << d;
+    const v2f p0 = UP ? shup(e0, sh) : shdn(e0, sh), p1 = UP ? shup(e1, sh) : shdn(e1, sh);
+    if (UP ? lane >= sh : lane + sh < 64) {
+      const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
+      e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
+      e0 = n0;
+    }
+  }
+  v2f s0 = splat(0.f), s1 = splat(0.f);  // state entering this wave's first block
+  if constexpr (XW) {
+    if (lane == (UP ? 63 : 0)) {
+      scr[2 * wave] = e0;
+      scr[2 * wave + 1] = e1;
+    }
+    __syncthreads();
+    const int src = UP ? wave - 1 : wave + 1;
+    if (src >= 0 && src < 4) {
+      s0 = scr[2 * src];
+      s1 = scr[2 * src + 1];
+      const int dist = UP ? lane : 63 - lane;  // blocks between this one and the source's
+      const float __attribute__((address_space(4))) *x = xw + 4 * dist;
+      const v2f n0 = vfma(splat(x[0]), s0, vfma(splat(x[1]), s1, e0));
+      e1 = vfma(splat(x[2]), s0, vfma(splat(x[3]), s1, e1));
+      e0 = n0;
+    }
+  }
+  v2f i0 = UP ? shup(e0, 1) : shdn(e0, 1), i1 = UP ? shup(e1, 1) : shdn(e1, 1);
+  if (lane == (UP ? 0 : 63)) {
+    i0 = s0;
+    i1 = s1;
+  }
+#pragma unroll
+  for (int c = 0; c < DCUT; ++c) {
+    const int k = UP ? c : B - 1 - c;
+    v[k] = vfma(splat(S.ct[c][0]), i0, vfma(splat(S.ct[c][1]), i1, v[k]));
+  }
+}
+
+template <int S, bool UP>
+__device__ __forceinline__ void ap_cascade(v2f (&a)[kPcApBlk], CT tab, int lane) {
+  sec_block<kPcApBlk, pc_ap_levels(S), pc_ap_dcut(S), UP, false, false, S>(a, tab, nullptr, lane, 0);
+  if constexpr (S + 1 < kPcAp) ap_cascade<S + 1, UP>(a, tab, lane);
+}
+
+constexpr int kApRow = kPcApBlk + 2;           // AP lane rows padded to 38 (b128 conflict-free)
+constexpr int kOutOff = 64 * kApRow;           // final outputs staged after the AP rows
+static_assert(kOutOff + kPcK2M <= kPcK2Span, "K2 LDS layout");
+static_assert(256 * 9 == 64 * kPcApBlk, "FIR gamma outputs = AP lane blocks");
+
+// One tile: outputs [m0, m0 + 2048), m0 = 2048 tile, from y2 over [2 m0 - 520, + 5376).
+__global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s, int64_t y2n,
+                                                      v2f *out, int64_t n3, CT tab) {
+  __shared__ v4f sp4[kPcK2Span / 2];
+  __shared__ v4f scr4[4 * 4];
+  const LP sp = (LP)sp4;
+  const LP scr = (LP)scr4;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t f = blockIdx.y, m0 = (int64_t)kPcK2M * blockIdx.x;
+  const int64_t g0 = 2 * m0 - kPcK2Left - kPcQ0;  // y2 entry of span sample 0
+  const v2f *yb = y2 + f * y2s;
+  for (int s = 2 * t; s < kPcK2Span; s += 512) {
+    const int64_t g = g0 + s;  // even: a pair is wholly inside or outside [0, y2n)
+    v4f w = v4f{0.f, 0.f, 0.f, 0.f};
+    if (g >= 0 && g < y2n) w = *(const v4f *)(yb + g);
+    *(LP4)(sp + s) = w;
+  }
+  __syncthreads();
+  v2f v[kPcOwnBlk];
+#pragma unroll
+  for (int k = 0; k < kPcOwnBlk; ++k) v[k] = sp[kPcOwnBlk * t + k];
+  // own-rate sections, causal then anticausal (warm-up: the span's first / last 330)
+  sec_block<kPcOwnBlk, pc_own_levels(0), kPcOwnBlk, true, true, true, 0>(v, tab, scr, lane, wave);
+  sec_block<kPcOwnBlk, pc_own_levels(1), kPcOwnBlk, true, true, true, 1>(v, tab, scr + 8, lane, wave);
+  sec_block<kPcOwnBlk, pc_own_levels(0), kPcOwnBlk, false, true, true, 0>(v, tab, scr + 16, lane, wave);
+  sec_block<kPcOwnBlk, pc_own_levels(1), kPcOwnBlk, false, true, true, 1>(v, tab, scr + 24, lane, wave);
+  __syncthreads();  // every thread has its block in registers
+#pragma unroll
+  for (int k = 0; k < kPcOwnBlk; ++k) sp[kPcOwnBlk * t + k] = v[k];
+  __syncthreads();
+  // FIR gamma: u3[m0 - 80 + k], k = 9t + r, from z2 local [2k + 332, 2k + 388]
+  v2f u[9];
+#pragma unroll
+  for (int r = 0; r < 9; ++r) u[r] = splat(0.f);
+  {
+    const LP zb = sp + 18 * t + (kPcK2Left - 2 * kPcApHalo) - (kPcG2 - 1) / 2;
+#pragma unroll
+    for (int p = 0; p < 37; ++p) {
+      const int j = 2 * p;
+      const v4f w = *(LP4)(zb + j);
+      const v2f x0 = lo2(w), x1 = hi2(w);
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        const int q = j - 2 * r;
+        if (q >= 0 && q < kPcG2) u[r] = vfma(splat(tab->g2[q]), x0, u[r]);
+        if (q + 1 >= 0 && q + 1 < kPcG2) u[r] = vfma(splat(tab->g2[q + 1]), x1, u[r]);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 9; ++r) sp[(t >> 2) * kApRow + 9 * (t & 3) + r] = u[r];
+  __syncthreads();
+  // output-rate sections on one wave: lane blocks of 36 (u3 index k = 36 lane + i)
+  if (wave == 0) {
+    v2f a[kPcApBlk];
+#pragma unroll
+    for (int q = 0; q < kPcApBlk / 2; ++q) {
+      const v4f w = *(LP4)(sp + lane * kApRow + 2 * q);
+      a[2 * q] = lo2(w);
+      a[2 * q + 1] = hi2(w);
+    }
+    ap_cascade<0, true>(a, tab, lane);
+    ap_cascade<0, false>(a, tab, lane);
+#pragma unroll
+    for (int i = 0; i < kPcApBlk; ++i) {
+      const int k = kPcApBlk * lane + i - kPcApHalo;
+      if (k >= 0 && k < kPcK2M) sp[kOutOff + k] = a[i];
+    }
+  }
+  __syncthreads();
+  v2f *ob = out + f * n3;
+  for (int s = t; s < kPcK2M; s += 256)
+    if (m0 + s < n3) ob[m0 + s] = sp[kOutOff + s];
+}
+
+// ---------------------------------------------------------------------------------- K3
+
+// out[m] += sum_k U[m][k] (sum_j V[j][k] x[j]): side 0 from the frame start, side 1 from
+// its end (x[j] = mixed input L-1-j, out index n3-1-m).  One block per frame and side.
+template <int DT, int FLIP>
+__global__ void __launch_bounds__(256) pc_edge_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3,
+                                                      const float *U0, const float *V0, int R0, int J0,
+                                                      int r0, const float *U1, const float *V1, int R1,
+                                                      int J1, int r1) {
+  __shared__ v2f red[4][kPcEdgeRank];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t f = blockIdx.x, L = in.len;
+  const int side = blockIdx.y;
+  const float *U = side ? U1 : U0, *V = side ? V1 : V0;
+  const int R = side ? R1 : R0, J = side ? J1 : J0, r = side ? r1 : r0;
+  const v2f *lor = lo_row(lo, in, f);
+  v2f acc[kPcEdgeRank];
+#pragma unroll
+  for (int k = 0; k < kPcEdgeRank; ++k) acc[k] = splat(0.f);
+  for (int j = t; j < J; j += 256) {
+    const int64_t n = side ? L - 1 - j : j;
+    const v2f x = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
+#pragma unroll
+    for (int k = 0; k < kPcEdgeRank; ++k)
+      if (k < r) acc[k] = vfma(splat(V[(int64_t)j * r + k]), x, acc[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kPcEdgeRank; ++k) {
+    v2f a = acc[k];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) a += shxor(a, d);
+    if (lane == 0) red[wave][k] = a;
+  }
+  __syncthreads();
+  if (t < R) {
+    v2f c = splat(0.f);
+    for (int k = 0; k < r; ++k)
+      c = vfma(splat(U[t * r + k]), red[0][k] + red[1][k] + red[2][k] + red[3][k], c);
+    const int64_t m = side ? n3 - 1 - t : t;
+    out[f * n3 + m] += c;
+  }
+}
+
+}  // namespace pc
+
+#define PC_LAUNCH2(KERNEL, DT, fl, ...)                                                         \
+  do {                                                                                           \
+    if (fl) hipLaunchKernelGGL((KERNEL<DT, 1>), __VA_ARGS__);                                    \
+    else hipLaunchKernelGGL((KERNEL<DT, 0>), __VA_ARGS__);                                       \
+  } while (0)
+#define PC_DISPATCH(KERNEL, in, ...)                                                             \
+  do {                                                                                           \
+    const bool fl = (in).flip != 0;                                                              \
+    switch ((in).dtype) {                                                                        \
+      case kInC64: PC_LAUNCH2(KERNEL, kInC64, fl, __VA_ARGS__); break;                           \
+      case kInC32H: PC_LAUNCH2(KERNEL, kInC32H, fl, __VA_ARGS__); break;                         \
+      case kInCU8: PC_LAUNCH2(KERNEL, kInCU8, fl, __VA_ARGS__); break;                           \
+      default: PC_LAUNCH2(KERNEL, kInF32R, fl, __VA_ARGS__); break;                              \
+    }                                                                                            \
+  } while (0)
+
+hipError_t launch_pc_fir(const InDesc &in, const float2 *lo, float2 *y2, int64_t y2_stride,
+                         int frames, const PcTab *tab, hipStream_t st) {
+  const int ntiles = (int)((pc_y2_len(in.len) + kPcK1Q - 1) / kPcK1Q);
+  const dim3 grid(ntiles, frames);
+  const pc::CT ct = (pc::CT)tab;
+  PC_DISPATCH(pc::pc_fir_kernel, in, grid, dim3(256), 0, st, in, (const v2f *)lo, (v2f *)y2,
+              y2_stride, ct);
+  return hipGetLastError();
+}
+
+hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int64_t n3,
+                          int frames, const PcTab *tab, hipStream_t st) {
+  const dim3 grid((unsigned)((n3 + kPcK2M - 1) / kPcK2M), frames);
+  hipLaunchKernelGGL(pc::pc_tail_kernel, grid, dim3(256), 0, st, (const v2f *)y2, y2_stride,
+                     y2_stride, (v2f *)out, n3, (pc::CT)tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_pc_edge(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
+                          const float *const U[2], const float *const V[2], const int R[2],
+                          const int J[2], const int r[2], hipStream_t st) {
+  const dim3 grid(frames, 2);
+  PC_DISPATCH(pc::pc_edge_kernel, in, grid, dim3(256), 0, st, in, (const v2f *)lo, (v2f *)out, n3,
+              U[0], V[0], R[0], J[0], r[0], U[1], V[1], R[1], J[1], r[1]);
+  return hipGetLastError();
+}
+
+}  // namespace zfft

@@ -132,6 +132,71 @@ constexpr int kXaRing = 4096;
 hipError_t launch_xa_fused(const InDesc &in, int D, const int64_t *n, const float2 *lo, bool mix,
                            float2 *ring, float2 *out, int frames, const XaTab *tab, hipStream_t st);
 
+// "PC" (polyphase cascade) decimator for zoom 8 (pc_kernels.hip, host tables pc_tables.cpp,
+// design model tools/pc_model.py).  The interior of the three zero-phase stages is, exactly,
+//   y1 = (g0 * x)|2, y2 = (g1 * y1)|2        FIRs (33, 49 taps): every all-pole factor of
+//                                            stages 0-1 moved to the output rate (polyphase)
+//   z2 = S(v) S(1/v) y2                      the two slowest sections of stage 2 at their own
+//                                            rate (fp32 conditioning), zero-phase
+//   u3 = (g2 * z2)|2                         FIR (57 taps)
+//   out = A(w) A(1/w) u3                     10 sections at the output rate (radius <= .765)
+// on the zero-extended frame; the frame ends (odd extension, sosfilt_zi states) add a
+// low-rank linear map of the first / last input samples onto the first / last outputs.
+// K1 = the two FIRs (independent tiles) -> y2 in device memory; K2 = the rest (independent
+// tiles with warm-up halos); K3 = the edge maps.
+constexpr int kPcStages = 3;              // zoom 8 only
+constexpr int kPcQ0 = -16;                // first y2 index of the model's support
+constexpr int kPcK1Q = 992;               // y2 outputs per K1 tile
+constexpr int kPcK1In = 4128;             // input samples per K1 tile (from 4 q_s - 64)
+constexpr int kPcK2M = 2048;              // outputs per K2 tile
+constexpr int kPcK2Span = 5376;           // y2 samples per K2 tile: 256 thread blocks of 21
+constexpr int kPcK2Left = 520;            // span starts at 2 m0 - 520
+constexpr int kPcOwnBlk = 21;             // own-rate samples per thread
+constexpr int kPcApBlk = 36;              // output-rate samples per lane (one wave)
+constexpr int kPcApHalo = 80;             // output-rate warm-up (0.765^80 < 1e-9)
+constexpr int kPcG0 = 33, kPcG1 = 49, kPcG2 = 57;
+constexpr int kPcOwn = 2, kPcAp = 10;
+constexpr int kPcEdgeR = 192, kPcEdgeJ = 1536, kPcEdgeRank = 16;  // edge map capacities
+// One second-order all-pole section y[t] = x[t] - a1 y[t-1] - a2 y[t-2] run over lane blocks
+// of B samples: state s = (y[t-1], y[t-2]); pw[d] = A^(B 2^d) (row-major 2x2) for the lane
+// scan; ct[t] = e0 A^(t+1): output t's response to the entering state.
+struct PcSec {
+  float a1, a2, pad_[2];
+  float pw[4][4];
+  float ct[kPcApBlk][2];
+};
+struct PcTab {
+  float g0[36], g1[52], g2[60];     // zero-phase FIR taps (centred)
+  PcSec own[kPcOwn];                // B = 21 (stage 2's sections 2, 3)
+  float own_x[kPcOwn][64][4];       // A^(21 (i + 1)) for lane i (cross-wave scan step)
+  PcSec ap[kPcAp];                  // B = 36, slowest first
+};
+// Scan levels and correction lengths the kernels are compiled for (checked by the builder).
+__host__ __device__ constexpr int pc_own_levels(int s) { return s == 0 ? 3 : 4; }
+__host__ __device__ constexpr int pc_ap_levels(int s) { return s == 0 ? 2 : s == 1 ? 1 : 0; }
+__host__ __device__ constexpr int pc_ap_dcut(int s) {
+  return s < 2 ? 36 : s == 2 ? 31 : s == 3 ? 28 : s == 4 ? 22 : s == 5 ? 16 : s == 6 ? 15
+       : s == 7 ? 12 : s == 8 ? 8 : 6;
+}
+// Frame-end maps, out[m] += sum_k U[m][k] (sum_j V[j][k] x[j]) (left: m, j from the start;
+// right: from the end), rank r.
+struct PcEdge {
+  int R = 0, J = 0, r = 0;
+  std::vector<float> U, V;         // R x r, J x r (row-major)
+};
+bool pc_build_tables(PcTab &tab);
+// side 0 = frame start, 1 = frame end (depends on L mod 8)
+bool pc_edge_map(int side, int lmod8, PcEdge &out);
+int64_t pc_y2_len(int64_t L);      // y2 entries per frame (from kPcQ0)
+hipError_t launch_pc_fir(const InDesc &in, const float2 *lo, float2 *y2, int64_t y2_stride,
+                         int frames, const PcTab *tab, hipStream_t st);
+hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int64_t n3,
+                          int frames, const PcTab *tab, hipStream_t st);
+// both frame ends in one launch: [0] = start, [1] = end
+hipError_t launch_pc_edge(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
+                          const float *const U[2], const float *const V[2], const int R[2],
+                          const int J[2], const int r[2], hipStream_t st);
+
 struct WelchGeom {
   int n_fft, log2n;
   int n_win;

@@ -10,6 +10,8 @@
 #include <cmath>
 #include <complex>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -397,10 +399,15 @@ struct zfft_plan {
   int n_marks = 0;
   int sched_frames = 0;  // > 0 inside a batched zfft_process: the whole call's frame count
   int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows,
-                // 3 XA tiles (all-pole + FIR + half-rate all-pole)
+                // 3 XA tiles (all-pole + FIR + half-rate all-pole), 4 PC (polyphase cascade,
+                // zoom 8)
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
   DevBuf edge, xk, xa_tab, tws, means, z4, xa_ring, winf;
   int xa_fuse = 0;  // XA stages per launch (0 auto: kXaFuseAuto)
+  DevBuf pc_tab, pc_edge;  // PC decimator: PcTab; edge maps U0 V0 U1 V1 (floats)
+  int pc_lm = -1;          // L mod 8 of the right-edge map in pc_edge (-1: none)
+  int pc_R[2] = {}, pc_J[2] = {}, pc_r[2] = {};
+  size_t pc_off[4] = {};   // float offsets of U0 V0 U1 V1 in pc_edge
   // waterfall rendering: colormap LUT (host copy + device), levels
   uint8_t lut[256 * 4] = {};
   bool lut_ready = false;         // lut holds the chosen map (built on first use)
@@ -785,6 +792,96 @@ int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t
   return ZFFT_OK;
 }
 
+// PC decimator (pc_kernels.hip): zoom 8, frames long enough that the two frame ends'
+// maps do not meet (kPcMinL), grid y = frames.
+constexpr int64_t kPcMinL = 16384;
+bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
+  return p->K == kPcStages && L >= kPcMinL && frames <= 65535;
+}
+
+// Host copies of the PC tables: built once per process (the edge maps per L mod 8, on
+// first use: ~0.2 s each).
+const PcTab *pc_host_tab() {
+  static const std::unique_ptr<PcTab> t = [] {
+    std::unique_ptr<PcTab> x(new PcTab());
+    if (!pc_build_tables(*x)) x.reset();
+    return x;
+  }();
+  return t.get();
+}
+const PcEdge *pc_host_edge(int side, int lm) {
+  static std::mutex mu;
+  static std::unique_ptr<PcEdge> cache[9];  // [0..7] frame end by L mod 8, [8] frame start
+  std::lock_guard<std::mutex> lock(mu);
+  std::unique_ptr<PcEdge> &e = cache[side == 0 ? 8 : (lm & 7)];
+  if (!e) {
+    std::unique_ptr<PcEdge> x(new PcEdge());
+    if (pc_edge_map(side, lm & 7, *x)) e = std::move(x);
+  }
+  return e.get();
+}
+
+int ensure_pc(zfft_plan *p, int64_t L) {
+  if (!p->pc_tab.p) {
+    const PcTab *t = pc_host_tab();
+    if (!t) return fail(ZFFT_EHIP, "PC tables: scan depth or correction length too short");
+    hipError_t e = p->pc_tab.ensure(sizeof(PcTab));
+    if (e == hipSuccess) e = hipMemcpy(p->pc_tab.p, t, sizeof(PcTab), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "PC table upload");
+  }
+  const int lm = (int)(L & 7);
+  if (p->pc_lm == lm) return ZFFT_OK;
+  const PcEdge *e0 = pc_host_edge(0, 0), *e1 = pc_host_edge(1, lm);
+  if (!e0 || !e1) return fail(ZFFT_EHIP, "PC frame-end maps: support beyond the computed block");
+  int rc = quiesce(p);  // enqueued work may still read the old maps
+  if (rc) return rc;
+  const PcEdge *es[2] = {e0, e1};
+  std::vector<float> h;
+  for (int s = 0; s < 2; ++s) {
+    p->pc_R[s] = es[s]->R;
+    p->pc_J[s] = es[s]->J;
+    p->pc_r[s] = es[s]->r;
+    p->pc_off[2 * s] = h.size();
+    h.insert(h.end(), es[s]->U.begin(), es[s]->U.end());
+    p->pc_off[2 * s + 1] = h.size();
+    h.insert(h.end(), es[s]->V.begin(), es[s]->V.end());
+  }
+  hipError_t e = p->pc_edge.ensure(h.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(p->pc_edge.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "PC edge map upload");
+  p->pc_lm = lm;
+  return ZFFT_OK;
+}
+
+// PC path: K1 (FIRs) -> y2 (ping) -> K2 (own-rate sections, FIR, output-rate sections) ->
+// out (pong) -> K3 (frame-end maps, in place).
+int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vector<int64_t> &n,
+           const float2 **out, hipStream_t st) {
+  int rc = ensure_pc(p, L);
+  if (rc) return rc;
+  const int64_t n3 = n[p->K];
+  const int64_t y2s = (pc_y2_len(L) + kPcK1Q - 1) / kPcK1Q * kPcK1Q;
+  hipError_t e = p->ping.ensure((size_t)frames * y2s * sizeof(float2));
+  if (e == hipSuccess) e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+  const PcTab *tab = p->pc_tab.as<PcTab>();
+  e = launch_pc_fir(in, p->lo.as<float2>(), p->ping.as<float2>(), y2s, frames, tab, st);
+  if (e != hipSuccess) return hip_fail(e, "pc_fir launch");
+  mark(p, st, "pc_fir");
+  e = launch_pc_tail(p->ping.as<float2>(), y2s, p->pong.as<float2>(), n3, frames, tab, st);
+  if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
+  mark(p, st, "pc_tail");
+  const float *eb = p->pc_edge.as<float>();
+  const float *const U[2] = {eb + p->pc_off[0], eb + p->pc_off[2]};
+  const float *const V[2] = {eb + p->pc_off[1], eb + p->pc_off[3]};
+  e = launch_pc_edge(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, U, V, p->pc_R,
+                     p->pc_J, p->pc_r, st);
+  if (e != hipSuccess) return hip_fail(e, "pc_edge launch");
+  mark(p, st, "pc_edge");
+  *out = p->pong.as<float2>();
+  return ZFFT_OK;
+}
+
 int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
                   const std::vector<int64_t> &n, const float2 **out, hipStream_t st) {
   if (p->path == 3 && !xa_fits(p, L))
@@ -795,6 +892,12 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
   const int sf = std::max(frames, p->sched_frames);
+  if (p->path == 4) {
+    if (!pc_fits(p, L, frames))
+      return fail(ZFFT_EUNSUPPORTED, "PC decimator (path 4) needs zoom 8, frames of >= 16384 "
+                                     "samples and <= 65535 frames per call");
+    return run_pc(p, in, L, frames, n, out, st);
+  }
   if (p->path == 3 || (p->path == 0 && auto_xa(sf, L) && xa_fits(p, L)))
     return run_xa(p, in, frames, n, out, st);
   if (use_fused(p, L, sf)) return run_fused(p, in, L, frames, n, out, st);
@@ -1062,7 +1165,7 @@ int zfft_plan_destroy(zfft_plan *p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->in2, &p->yf, &p->ping, &p->pong, &p->rows,
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
-                    &p->tws, &p->means, &p->z4, &p->xa_ring, &p->winf})
+                    &p->tws, &p->means, &p->z4, &p->xa_ring, &p->winf, &p->pc_tab, &p->pc_edge})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->done_ev) (void)hipEventDestroy(p->done_ev);
@@ -1103,8 +1206,8 @@ int zfft_plan_timing(zfft_plan *p, int32_t enable) {
 }
 
 int zfft_plan_path(zfft_plan *p, int32_t path) {
-  if (!p || path < 0 || path > 3)
-    return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused) or 3 (XA tiles)");
+  if (!p || path < 0 || path > 4)
+    return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused), 3 (XA tiles) or 4 (PC)");
   p->path = path;
   return ZFFT_OK;
 }

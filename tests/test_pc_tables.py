@@ -1,0 +1,127 @@
+"""CPU checks of the PC decimator's host tables (pc_tables.cpp, no GPU needed):
+
+* the FIR taps equal the polyphase factorisation rebuilt here from scipy's cheby1 sections;
+* the LTI model those tables describe plus the library's frame-end maps reproduces
+  3 x scipy.signal.decimate(x, 2) -- the reference's zoomfft at zoom 8
+  (pypanadapter_spectrum.py:2096-2098) -- in float64, for every L mod 8.
+
+The model is rebuilt here independently (numpy convolutions + scipy sosfilt of the same pole
+moves) so this pins the tables the kernels read, not the library against itself."""
+import ctypes
+
+import numpy as np
+import pytest
+import scipy.signal as ss
+
+SOS = ss.cheby1(8, 0.05, 0.4, output="sos")
+
+
+def _lib():
+    from pypanadapter_amd import _lib as L, build
+    build.build()
+    lib = L.load()
+    f = lib.zfft__pc_tables
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    f.restype = ctypes.c_int
+    return f
+
+
+def _call(what, arg=0):
+    f = _lib()
+    buf = np.zeros(1 << 20, np.float32)
+    n = f(what, arg, buf.ctypes.data, buf.size)
+    assert n > 0, (what, arg, n)
+    return buf[:n].astype(np.float64)
+
+
+def _neg(p):
+    p = p.copy()
+    p[1::2] *= -1
+    return p
+
+
+def _conv(*ps):
+    r = np.array([1.0])
+    for p in ps:
+        r = np.convolve(r, p)
+    return r
+
+
+def _secs():
+    a1, a2 = SOS[:, 4].copy(), SOS[:, 5].copy()
+    out = [(a1, a2)]
+    for _ in range(3):
+        a1, a2 = 2 * a2 - a1 ** 2, a2 ** 2
+        out.append((a1, a2))
+    return out
+
+
+def _poly(a1, a2, idx):
+    return _conv(*[np.array([1.0, a1[i], a2[i]]) for i in idx])
+
+
+def _model():
+    s = _secs()
+    n9 = SOS[0, 0] * np.array([1, 8, 28, 56, 70, 56, 28, 8, 1.0])
+    f0 = _conv(n9, _neg(_poly(*s[0], range(4))))
+    f1 = _conv(n9, _neg(_poly(*s[1], range(4))), _neg(_poly(*s[0], range(4))))
+    f2 = _conv(n9, _neg(_poly(*s[2], range(4))), _neg(_poly(*s[1], range(4))), _neg(_poly(*s[0], [0, 1])))
+    g = [np.convolve(f, f[::-1]) for f in (f0, f1, f2)]
+    own = [(s[0][0][i], s[0][1][i]) for i in (2, 3)]
+    ap = [(s[3][0][i], s[3][1][i]) for i in range(4)] + [(s[2][0][i], s[2][1][i]) for i in range(4)] + \
+         [(s[1][0][i], s[1][1][i]) for i in (0, 1)]
+    return g, own, ap
+
+
+def _run_model(x, g, own, ap):
+    pad = 4096
+    y = np.concatenate([np.zeros(pad), x, np.zeros(pad)])
+    for r in range(3):
+        if r == 2:
+            so = np.array([[1, 0, 0, 1, a1, a2] for a1, a2 in own])
+            y = ss.sosfilt(so, ss.sosfilt(so, y)[::-1])[::-1]
+        c = (len(g[r]) - 1) // 2
+        y = np.convolve(y, g[r])[c::2][:len(y) // 2]
+    sa = np.array([[1, 0, 0, 1, a1, a2] for a1, a2 in ap])
+    y = ss.sosfilt(sa, ss.sosfilt(sa, y)[::-1])[::-1]
+    n3 = len(x)
+    for _ in range(3):
+        n3 = (n3 + 1) // 2
+    return y[pad // 8:pad // 8 + n3]
+
+
+def test_pc_fir_taps_match_polyphase_factorisation():
+    g, _, _ = _model()
+    taps = _call(0)
+    want = np.concatenate(g)
+    assert taps.size == want.size == 33 + 49 + 57
+    np.testing.assert_allclose(taps, want, rtol=0, atol=4e-8 * np.abs(want).max())
+    for k, gg in enumerate(g):  # zero phase: symmetric taps
+        np.testing.assert_allclose(gg, gg[::-1], atol=1e-15)
+
+
+def _edge(side, lm):
+    v = _call(2 + side, lm)
+    R, J, r = int(v[0]), int(v[1]), int(v[2])
+    U = v[3:3 + R * r].reshape(R, r)
+    V = v[3 + R * r:3 + R * r + J * r].reshape(J, r)
+    return U @ V.T
+
+
+@pytest.mark.parametrize("L", [16384, 16385, 16386, 16387, 20004, 20005, 20006, 20007])
+def test_pc_model_plus_edge_maps_is_reference_decimate(L):
+    g, own, ap = _model()
+    rng = np.random.default_rng(L)
+    x = rng.standard_normal(L) + 1j * rng.standard_normal(L)
+    x += 3 * np.exp(2j * np.pi * 0.013 * np.arange(L))
+    ref = x
+    for _ in range(3):
+        ref = ss.decimate(ref, 2)
+    out = _run_model(x, g, own, ap)
+    inner = np.abs(out - ref)[200:-200].max() / np.abs(ref).max()
+    assert inner < 1e-12, inner        # the pole moves are exact in the interior
+    CL, CR = _edge(0, L % 8), _edge(1, L % 8)
+    out[:CL.shape[0]] += CL @ x[:CL.shape[1]]
+    out[len(out) - CR.shape[0]:] += (CR @ x[::-1][:CR.shape[1]])[::-1]
+    err = np.abs(out - ref).max() / np.abs(ref).max()
+    assert err < 2e-7, err             # fp32 storage of the rank-~10 maps

@@ -1,5 +1,6 @@
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r03blk; mkdir -p $O
-timeout -k 10 300 python3 tools/dbg/single_frame_blocks.py > $O/blk.log 2>&1 || { tail -5 $O/blk.log; exit 1; }
-cat $O/blk.log
+O=gpurun_out/r04a; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_pc.py -x -v --timeout 300 --timeout-method thread > $O/pc_tests.log 2>&1; rc=$?
+tail -30 $O/pc_tests.log
+exit $rc
