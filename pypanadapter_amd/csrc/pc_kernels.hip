@@ -17,6 +17,18 @@
 // Intermediates: only y2 (rate 1/4, 8 B per 4 input samples) goes through device memory.
 #include "zfft_device.h"
 
+// Diagnostic builds only (ZFFT_DIAG=1, never set by build.py): PC_KO timing knockouts with
+// wrong results by design -- 1 own-rate sections, 2 FIR gamma, 4 output-rate sections,
+// 8 K1's LO mix (and its table loads).
+#ifndef ZFFT_DIAG
+#define ZFFT_DIAG 0
+#endif
+#if ZFFT_DIAG && defined(PC_KO)
+constexpr int kKo = PC_KO;
+#else
+constexpr int kKo = 0;
+#endif
+
 namespace zfft {
 namespace pc {
 
@@ -96,14 +108,22 @@ __global__ void __launch_bounds__(256) pc_fir_kernel(InDesc in, const v2f *lo, v
   const int64_t xs = 4 * ((int64_t)kPcQ0 + (int64_t)kPcK1Q * tile) - 64;
   const v2f *lor = lo_row(lo, in, f);
   if (xs >= 0 && xs + kPcK1In <= L) {
+    // LO factor lo[n0 + 2t + j] = lo[n0] lo[2t + j] / sqrt 2 (the table is an exact
+    // exponential): one uniform entry per 512 samples instead of a table stream beside the
+    // input (which cost 13 % of the kernel, profiles/r04c)
+    const v4f lane_lo = *(const v4f *)(lor + 2 * t) * (float)M_SQRT1_2;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const int s = 2 * t + 512 * i;
       if (i == 8 && t >= (kPcK1In - 4096) / 2) break;
       v2f a, b;
       load_pair<DT, FLIP>(in, f, xs + s, a, b);
-      const v4f l = *(const v4f *)(lor + xs + s);
-      *(LP4)(xl + xidx(s)) = cat(cmul2(a, lo2(l)), cmul2(b, hi2(l)));
+      if constexpr (kKo & 8) {
+        *(LP4)(xl + xidx(s)) = cat(a, b);
+      } else {
+        const v2f c = lor[xs + 512 * i];  // uniform
+        *(LP4)(xl + xidx(s)) = cat(cmul2(a, cmul2(c, lo2(lane_lo))), cmul2(b, cmul2(c, hi2(lane_lo))));
+      }
     }
   } else {
     for (int s = t; s < kPcK1In; s += 256) {
@@ -162,14 +182,31 @@ __global__ void __launch_bounds__(256) pc_fir_kernel(InDesc in, const v2f *lo, v
 
 // ---------------------------------------------------------------------------------- K2
 
+// Whole-wave DPP shift by one lane toward higher (UP, wave_shr:1) or lower lanes
+// (wave_shl:1); the lane without a source reads 0.
+template <bool UP>
+__device__ __forceinline__ v2f wshift(v2f v) {
+  constexpr int ctrl = UP ? 0x138 : 0x130;
+  return v2f{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.x), ctrl, 0xF, 0xF, false)),
+             __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.y), ctrl, 0xF, 0xF, false))};
+}
+template <bool UP, int N>
+__device__ __forceinline__ v2f wshiftn(v2f v) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v = wshift<UP>(v);
+  return v;
+}
+
 // One all-pole section over this lane's block v[0..B) in time order (UP) or reversed (!UP),
-// the neighbouring lane blocks of the wave adjacent in time; XW: the 4 waves of the block
-// continue each other (cross-wave step through scr, which holds 4 waves x 2 states).
+// the wave's lane blocks adjacent in time: zero-state run, Kogge-Stone over lanes on DPP
+// shifts (levels d: + A^(B 2^d) times the state 2^d lanes back), the entering state's
+// response ct[t] for t < DCUT.  XW: the block's 4 waves continue each other (one
+// cross-wave step through scr: 4 waves x 2 states); otherwise lane 0 (UP) / 63 enters
+// from a zero state.
 template <int B, int LEV, int DCUT, bool UP, bool XW, bool OWN, int SI>
 __device__ __forceinline__ void sec_block(v2f (&v)[B], CT tab0, LP scr, int lane, int wave) {
   const CT tab = fresh(tab0);
   CS S = OWN ? tab->own[SI] : tab->ap[SI];
-  const float __attribute__((address_space(4))) *xw = &tab->own_x[OWN ? SI : 0][0][0];
   const v2f na1 = splat(-S.a1), na2 = splat(-S.a2);
   v2f y1 = splat(0.f), y2 = splat(0.f);
 #pragma unroll
@@ -183,13 +220,14 @@ __device__ __forceinline__ void sec_block(v2f (&v)[B], CT tab0, LP scr, int lane
   v2f e0 = y1, e1 = y2;  // exit state from a zero entering state
 #pragma unroll
   for (int d = 0; d < LEV; ++d) {
-    const int sh = 1 << d;
-    const v2f p0 = UP ? shup(e0, sh) : shdn(e0, sh), p1 = UP ? shup(e1, sh) : shdn(e1, sh);
-    if (UP ? lane >= sh : lane + sh < 64) {
-      const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
-      e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
-      e0 = n0;
-    }
+    v2f p0, p1;
+    if (d == 0) p0 = wshiftn<UP, 1>(e0), p1 = wshiftn<UP, 1>(e1);
+    else if (d == 1) p0 = wshiftn<UP, 2>(e0), p1 = wshiftn<UP, 2>(e1);
+    else if (d == 2) p0 = wshiftn<UP, 4>(e0), p1 = wshiftn<UP, 4>(e1);
+    else p0 = wshiftn<UP, 8>(e0), p1 = wshiftn<UP, 8>(e1);
+    const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
+    e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
+    e0 = n0;
   }
   v2f s0 = splat(0.f), s1 = splat(0.f);  // state entering this wave's first block
   if constexpr (XW) {
@@ -203,13 +241,13 @@ __device__ __forceinline__ void sec_block(v2f (&v)[B], CT tab0, LP scr, int lane
       s0 = scr[2 * src];
       s1 = scr[2 * src + 1];
       const int dist = UP ? lane : 63 - lane;  // blocks between this one and the source's
-      const float __attribute__((address_space(4))) *x = xw + 4 * dist;
+      const float __attribute__((address_space(4))) *x = &tab->own_x[OWN ? SI : 0][dist][0];
       const v2f n0 = vfma(splat(x[0]), s0, vfma(splat(x[1]), s1, e0));
       e1 = vfma(splat(x[2]), s0, vfma(splat(x[3]), s1, e1));
       e0 = n0;
     }
   }
-  v2f i0 = UP ? shup(e0, 1) : shdn(e0, 1), i1 = UP ? shup(e1, 1) : shdn(e1, 1);
+  v2f i0 = wshift<UP>(e0), i1 = wshift<UP>(e1);
   if (lane == (UP ? 0 : 63)) {
     i0 = s0;
     i1 = s1;
@@ -227,12 +265,15 @@ __device__ __forceinline__ void ap_cascade(v2f (&a)[kPcApBlk], CT tab, int lane)
   if constexpr (S + 1 < kPcAp) ap_cascade<S + 1, UP>(a, tab, lane);
 }
 
-constexpr int kApRow = kPcApBlk + 2;           // AP lane rows padded to 38 (b128 conflict-free)
-constexpr int kOutOff = 64 * kApRow;           // final outputs staged after the AP rows
+constexpr int kU3 = 256 * 9;                   // FIR gamma outputs per tile (9 per thread)
+constexpr int kU3Base = 128;                    // u3 index k <-> output m0 - 128 + k
+constexpr int kApWave = 64 * kPcApBlk;          // output-rate samples per wave (512 + halos)
+constexpr int kOutOff = kU3;                    // final outputs staged after u3
 static_assert(kOutOff + kPcK2M <= kPcK2Span, "K2 LDS layout");
-static_assert(256 * 9 == 64 * kPcApBlk, "FIR gamma outputs = AP lane blocks");
+static_assert(kApWave == kPcK2M / 4 + 2 * kPcApHalo, "one wave per quarter tile with its halos");
+static_assert(kU3Base - kPcApHalo + 3 * (kPcK2M / 4) + kApWave <= kU3, "u3 covers the waves");
 
-// One tile: outputs [m0, m0 + 2048), m0 = 2048 tile, from y2 over [2 m0 - 520, + 5376).
+// One tile: outputs [m0, m0 + 2048), m0 = 2048 tile, from y2 over [2 m0 - 560, + 5376).
 __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s, int64_t y2n,
                                                       v2f *out, int64_t n3, CT tab) {
   __shared__ v4f sp4[kPcK2Span / 2];
@@ -254,20 +295,25 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
 #pragma unroll
   for (int k = 0; k < kPcOwnBlk; ++k) v[k] = sp[kPcOwnBlk * t + k];
   // own-rate sections, causal then anticausal (warm-up: the span's first / last 330)
-  sec_block<kPcOwnBlk, pc_own_levels(0), kPcOwnBlk, true, true, true, 0>(v, tab, scr, lane, wave);
-  sec_block<kPcOwnBlk, pc_own_levels(1), kPcOwnBlk, true, true, true, 1>(v, tab, scr + 8, lane, wave);
-  sec_block<kPcOwnBlk, pc_own_levels(0), kPcOwnBlk, false, true, true, 0>(v, tab, scr + 16, lane, wave);
-  sec_block<kPcOwnBlk, pc_own_levels(1), kPcOwnBlk, false, true, true, 1>(v, tab, scr + 24, lane, wave);
+  if constexpr (!(kKo & 1)) {
+    sec_block<kPcOwnBlk, pc_own_levels(0), kPcOwnBlk, true, true, true, 0>(v, tab, scr, lane, wave);
+    sec_block<kPcOwnBlk, pc_own_levels(1), kPcOwnBlk, true, true, true, 1>(v, tab, scr + 8, lane, wave);
+    sec_block<kPcOwnBlk, pc_own_levels(0), kPcOwnBlk, false, true, true, 0>(v, tab, scr + 16, lane, wave);
+    sec_block<kPcOwnBlk, pc_own_levels(1), kPcOwnBlk, false, true, true, 1>(v, tab, scr + 24, lane, wave);
+  }
   __syncthreads();  // every thread has its block in registers
 #pragma unroll
   for (int k = 0; k < kPcOwnBlk; ++k) sp[kPcOwnBlk * t + k] = v[k];
   __syncthreads();
-  // FIR gamma: u3[m0 - 80 + k], k = 9t + r, from z2 local [2k + 332, 2k + 388]
+  // FIR gamma: u3 index k = 9t + r (output m0 - 128 + k) from z2 local [2k + 276, 2k + 332]
   v2f u[9];
 #pragma unroll
   for (int r = 0; r < 9; ++r) u[r] = splat(0.f);
-  {
-    const LP zb = sp + 18 * t + (kPcK2Left - 2 * kPcApHalo) - (kPcG2 - 1) / 2;
+  if constexpr (kKo & 2) {
+#pragma unroll
+    for (int r = 0; r < 9; ++r) u[r] = sp[18 * t + 2 * r + 304];
+  } else {
+    const LP zb = sp + 18 * t + (kPcK2Left - 2 * kU3Base) - (kPcG2 - 1) / 2;
 #pragma unroll
     for (int p = 0; p < 37; ++p) {
       const int j = 2 * p;
@@ -283,23 +329,25 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 9; ++r) sp[(t >> 2) * kApRow + 9 * (t & 3) + r] = u[r];
+  for (int r = 0; r < 9; ++r) sp[9 * t + r] = u[r];
   __syncthreads();
-  // output-rate sections on one wave: lane blocks of 36 (u3 index k = 36 lane + i)
-  if (wave == 0) {
+  // output-rate sections: wave q takes outputs [512 q, + 512) with 96-sample halos, u3
+  // index k = 32 + 512 q + 11 lane + i
+  {
     v2f a[kPcApBlk];
+    const int k0 = kU3Base - kPcApHalo + (kPcK2M / 4) * wave + kPcApBlk * lane;
 #pragma unroll
-    for (int q = 0; q < kPcApBlk / 2; ++q) {
-      const v4f w = *(LP4)(sp + lane * kApRow + 2 * q);
-      a[2 * q] = lo2(w);
-      a[2 * q + 1] = hi2(w);
+    for (int i = 0; i < kPcApBlk; ++i) a[i] = sp[k0 + i];
+    if constexpr (!(kKo & 4)) {
+      ap_cascade<0, true>(a, tab, lane);
+      ap_cascade<0, false>(a, tab, lane);
     }
-    ap_cascade<0, true>(a, tab, lane);
-    ap_cascade<0, false>(a, tab, lane);
+    __syncthreads();  // every wave has read its (overlapping) u3 range
 #pragma unroll
     for (int i = 0; i < kPcApBlk; ++i) {
-      const int k = kPcApBlk * lane + i - kPcApHalo;
-      if (k >= 0 && k < kPcK2M) sp[kOutOff + k] = a[i];
+      const int k = k0 + i - kU3Base;  // output index within the tile
+      const int q = k - (kPcK2M / 4) * wave;
+      if (q >= 0 && q < kPcK2M / 4) sp[kOutOff + k] = a[i];
     }
   }
   __syncthreads();

@@ -122,16 +122,16 @@ bool sec_tables(double a1, double a2, int B, int levels, int dcut, PcSec &s) {
   while (std::pow(r, (double)B * reach) > 1e-9) ++reach;
   const int need_levels = reach > 1 ? (int)std::ceil(std::log2((double)reach)) : 0;
   if (need_levels > levels) return false;
-  double mx = 0, row[kPcApBlk][2];
+  double mx = 0, row[kPcCt][2];
   M2 P = {{-a1, -a2}, {1.0, 0.0}};
-  for (int t = 0; t < kPcApBlk; ++t) {
+  for (int t = 0; t < kPcCt; ++t) {
     row[t][0] = P[0][0];
     row[t][1] = P[0][1];
     mx = std::max(mx, std::max(std::fabs(P[0][0]), std::fabs(P[0][1])));
     mul2(A, P, P);
   }
   int last = 0;
-  for (int t = 0; t < kPcApBlk; ++t) {
+  for (int t = 0; t < kPcCt; ++t) {
     if (t < B && std::max(std::fabs(row[t][0]), std::fabs(row[t][1])) > 1e-10 * mx) last = t + 1;
     s.ct[t][0] = (float)row[t][0];
     s.ct[t][1] = (float)row[t][1];

@@ -150,34 +150,34 @@ constexpr int kPcK1Q = 992;               // y2 outputs per K1 tile
 constexpr int kPcK1In = 4128;             // input samples per K1 tile (from 4 q_s - 64)
 constexpr int kPcK2M = 2048;              // outputs per K2 tile
 constexpr int kPcK2Span = 5376;           // y2 samples per K2 tile: 256 thread blocks of 21
-constexpr int kPcK2Left = 520;            // span starts at 2 m0 - 520
+constexpr int kPcK2Left = 560;            // span starts at 2 m0 - 560
 constexpr int kPcOwnBlk = 21;             // own-rate samples per thread
-constexpr int kPcApBlk = 36;              // output-rate samples per lane (one wave)
-constexpr int kPcApHalo = 80;             // output-rate warm-up (0.765^80 < 1e-9)
+constexpr int kPcApBlk = 11;              // output-rate samples per lane (each wave a quarter)
+constexpr int kPcApHalo = 96;             // output-rate warm-up per wave (0.765^96 < 1e-11)
 constexpr int kPcG0 = 33, kPcG1 = 49, kPcG2 = 57;
 constexpr int kPcOwn = 2, kPcAp = 10;
 constexpr int kPcEdgeR = 192, kPcEdgeJ = 1536, kPcEdgeRank = 16;  // edge map capacities
 // One second-order all-pole section y[t] = x[t] - a1 y[t-1] - a2 y[t-2] run over lane blocks
 // of B samples: state s = (y[t-1], y[t-2]); pw[d] = A^(B 2^d) (row-major 2x2) for the lane
 // scan; ct[t] = e0 A^(t+1): output t's response to the entering state.
+constexpr int kPcCt = 24;                 // zero-input response rows (>= both block lengths)
 struct PcSec {
   float a1, a2, pad_[2];
   float pw[4][4];
-  float ct[kPcApBlk][2];
+  float ct[kPcCt][2];
 };
 struct PcTab {
   float g0[36], g1[52], g2[60];     // zero-phase FIR taps (centred)
   PcSec own[kPcOwn];                // B = 21 (stage 2's sections 2, 3)
   float own_x[kPcOwn][64][4];       // A^(21 (i + 1)) for lane i (cross-wave scan step)
-  PcSec ap[kPcAp];                  // B = 36, slowest first
+  PcSec ap[kPcAp];                  // B = 11, slowest first
 };
 // Scan levels and correction lengths the kernels are compiled for (checked by the builder).
 __host__ __device__ constexpr int pc_own_levels(int s) { return s == 0 ? 3 : 4; }
-__host__ __device__ constexpr int pc_ap_levels(int s) { return s == 0 ? 2 : s == 1 ? 1 : 0; }
-__host__ __device__ constexpr int pc_ap_dcut(int s) {
-  return s < 2 ? 36 : s == 2 ? 31 : s == 3 ? 28 : s == 4 ? 22 : s == 5 ? 16 : s == 6 ? 15
-       : s == 7 ? 12 : s == 8 ? 8 : 6;
+__host__ __device__ constexpr int pc_ap_levels(int s) {
+  return s == 0 ? 3 : s <= 3 ? 2 : s <= 6 ? 1 : 0;
 }
+__host__ __device__ constexpr int pc_ap_dcut(int s) { return s < 8 ? kPcApBlk : s == 8 ? 8 : 6; }
 // Frame-end maps, out[m] += sum_k U[m][k] (sum_j V[j][k] x[j]) (left: m, j from the start;
 // right: from the end), rank r.
 struct PcEdge {
