@@ -39,7 +39,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "IQ Msamples/s + waterfall lines/s @ N_FFT=4096 zoom=8; % HBM roofline"
+def metric_of(n_fft: int, zoom: int) -> str:
+    """BASELINE.json's metric string (cfg2's N_FFT=4096 zoom=8), with the config's own N/zoom."""
+    return f"IQ Msamples/s + waterfall lines/s @ N_FFT={n_fft} zoom={zoom}; % HBM roofline"
+
+
+METRIC = metric_of(4096, 8)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 CONFIGS = {
@@ -60,13 +65,42 @@ IN_BYTES = {"complex64": 8, "complex32": 4, "cu8": 2}
 TONES = ((0.31, 1.0), (-0.57, 0.1))
 # plan launch name -> kernel-name prefix in the rocprofv3 / PMC summaries
 KERNEL_OF = {"xa_stage_mix": "xa_stage_kernel<32, true", "xa_stage": "xa_stage_kernel<32, false",
-             "xa_fused_mix": "xa_fused_kernel<true", "xa_fused": "xa_fused_kernel<false",
+             "pc_fir": "pc_fir_kernel", "pc_tail": "pc_tail_kernel", "pc_edge": "pc_edge_kernel",
              "welch_rows": "welch_", "welch4": "welch4_"}
 
 
 def alg_bytes_per_line(bps: int, L: int, W: int) -> int:
     """bps*L of IQ in + 4*W row out + 4*W waterfall ring row."""
     return bps * L + 8 * W
+
+
+def stage_lengths(L: int, zoom: int) -> list:
+    n = [L]
+    while zoom > 1:
+        n.append((n[-1] + 1) // 2)
+        zoom //= 2
+    return n
+
+
+def own_bytes_per_frame(name: str, bps: int, L: int, zoom: int, W: int, stage: int) -> int | None:
+    """A launch's OWN minimal bytes per frame: what it must read and write (its input and its
+    output arrays, intermediates included when they are its input or output) -- the basis of
+    kernels_roofline.  None for the blocked schedules (FGI intermediates, several passes)."""
+    n = stage_lengths(L, zoom)
+    if name == "pc_fir":  # IQ in, y2 (rate 1/4 from q = -16, complex64) out
+        y2 = ((L + 15) // 2 + 24) // 2 + 17
+        return bps * L + 8 * y2
+    if name == "pc_tail":
+        y2 = ((L + 15) // 2 + 24) // 2 + 17
+        return 8 * y2 + 8 * n[-1]
+    if name == "pc_edge":  # ~1070 IQ samples at each end in, ~160 outputs read and written
+        return bps * 2 * 1100 + 16 * 2 * 170
+    if name in ("xa_stage_mix", "xa_stage"):
+        k = stage
+        return (bps if k == 0 else 8) * n[k] + 8 * n[k + 1]
+    if name in ("welch_rows", "welch4"):
+        return 8 * n[-1] + 4 * W
+    return None
 
 
 # ----------------------------------------------------------------------------- CPU leg
@@ -303,6 +337,51 @@ def end_to_end(torch, args, cfg, x_dev, dev):
                        "frac_of_pcie_bound": round(rate / bound, 3)}
         del host, xe
     out["streaming_pinned"] = stream
+    out["display"] = display_timing(dev)
+    return out
+
+
+def display_timing(dev, widths=(512, 8192), lines=12) -> dict:
+    """The display side SURVEY §8f-2 exists for, per waterfall line: the facade's
+    `image_update(psd)` (device ring push, O(W)) then either `render()` (RGBA8 on the device +
+    D2H, what pyqtgraph's setImage turns the image into, S:1664) or `img_array` (the float64
+    image materialised on the host every line, the pre-r04 INTEGRATION.md binding); beside
+    them the reference's own `Waterfall.image_update` (oracle/scipy_path.py: full-image
+    np.roll per line, S:1638-1664) on the CPU."""
+    import numpy as np
+    from oracle.scipy_path import Waterfall as RefWaterfall
+    from pypanadapter_amd import Waterfall
+    out = {}
+    rng = np.random.default_rng(5)
+    for W in widths:
+        rows = rng.uniform(-200.0, -110.0, (lines + 2, W))
+        wf = Waterfall(scroll=1, device=dev.index)
+        res = {}
+        for what in ("push", "push_render", "push_img_array"):
+            ts = []
+            for k in range(lines + 2):
+                r = rows[k].astype(np.float32)
+                t0 = time.perf_counter()
+                wf.image_update(r)
+                if what == "push_render":
+                    wf.render()
+                elif what == "push_img_array":
+                    _ = wf.img_array
+                # "push" alone: zfft_waterfall_push synchronises its stream before returning
+                if k >= 2:
+                    ts.append((time.perf_counter() - t0) * 1e3)
+            res[what + "_ms_per_line"] = round(float(np.median(ts)), 3)
+        ref = RefWaterfall()
+        ts = []
+        for k in range(lines + 2):
+            t0 = time.perf_counter()
+            ref.image_update(rows[k].copy(), 1)
+            if k >= 2:
+                ts.append((time.perf_counter() - t0) * 1e3)
+        res["reference_cpu_image_update_ms_per_line"] = round(float(np.median(ts)), 3)
+        res["H"] = W // 4
+        out[f"W{W}"] = res
+        wf.close()
     return out
 
 
@@ -319,9 +398,7 @@ def main():
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--warm", type=int, default=0)
     ap.add_argument("--path", type=int, default=0,
-                    help="0 auto, 1 exact order, 2 fused interior, 3 XA tiles")
-    ap.add_argument("--fuse", type=int, default=0,
-                    help="XA stages per launch: 0 auto, 1 one per stage, 2-3 fused (A/B runs)")
+                    help="0 auto, 1 exact order, 2 fused interior, 3 XA tiles, 4 PC cascade")
     ap.add_argument("--welch", type=int, default=0,
                     help="Welch kernel: 0 auto, 1 one workgroup per frame, 2 four-step (A/B runs)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -363,15 +440,16 @@ def main():
     if args.dry_run and os.environ.get("BENCH_DRY_RUN_FAIL_RANK") == str(rank):
         sys.exit(3)  # launcher test: a rank that dies before the barrier
     if args.dry_run:  # the launcher's contract without touching a GPU
-        me = torch.tensor([rank, local, world, os.getpid()], dtype=torch.int64)
-        allr = [torch.zeros(4, dtype=torch.int64) for _ in range(world)] if dist else [me]
+        # plan_device: the GPU this rank's plan and streams would use (cuda:LOCAL_RANK)
+        me = torch.tensor([rank, local, world, os.getpid(), local], dtype=torch.int64)
+        allr = [torch.zeros(5, dtype=torch.int64) for _ in range(world)] if dist else [me]
         if dist:
             dist.all_gather(allr, me)
             dist.barrier()
             dist.destroy_process_group()
         if rank == 0:
             print(json.dumps({"dry_run": True, "world": world,
-                              "ranks": [dict(zip(("rank", "local_rank", "world", "pid"), map(int, r)))
+                              "ranks": [dict(zip(("rank", "local_rank", "world", "pid", "plan_device"), map(int, r)))
                                         for r in allr]}))
         return
     torch.cuda.set_device(local)
@@ -399,8 +477,6 @@ def main():
         plan.set_path(args.path)
     if args.welch:
         plan.set_welch(args.welch)
-    if args.fuse:
-        plan.set_fuse(args.fuse)
     stream = torch.cuda.Stream(dev)  # a real stream: the null stream's handle (0) would be
     torch.cuda.set_stream(stream)    # read by the C-ABI as HIP's default stream
     sp = stream.cuda_stream
@@ -485,26 +561,38 @@ def main():
     alg_step = F * alg_bytes_per_line(bps, L, W)
     ev_ms_step = ev_max / steps * 1e3
     path_gbs = alg_step / (ev_ms_step / 1e3) / 1e9
-    dominant = max(kernels, key=lambda k: kernels[k]) if kernels else None
     traffic_j, traffic_status = stamped_profile(
         os.path.join(ROOT, "profiles", f"traffic_{args.config}.json"), F, args.in_dtype)
     sq_j, sq_status = stamped_profile(os.path.join(ROOT, "profiles", f"sq_{args.config}.json"), F,
                                       args.in_dtype)
-    default_sched = not (args.path or args.welch or args.block or args.warm or args.fuse)
-    dom_traffic = step_traffic = valu = None
-    if dominant is not None and default_sched:
-        pref = KERNEL_OF.get(dominant.split(":", 1)[1], "?")
-        if traffic_j:
-            step_traffic = traffic_j.get("hbm_bytes_per_step")
-            dom_traffic = sum(v["hbm_bytes_per_step_fetch_x2"] for k, v in traffic_j["per_kernel"].items()
-                              if k.startswith(pref)) or None
-        if sq_j:
-            vk = [v for k, v in sq_j["per_kernel"].items() if k.startswith(pref)]
-            valu = vk[0].get("valu_busy") if vk else None
-    dom_ms = kernels.get(dominant) if dominant else None
-    dom_gbs = alg_step / (dom_ms / 1e3) / 1e9 if dom_ms else None
+    default_sched = not (args.path or args.welch or args.block or args.warm)
+    step_traffic = None
+    if traffic_j and default_sched:
+        step_traffic = traffic_j.get("hbm_bytes_per_step")
+    # per-launch component rooflines, each priced on its OWN input + output bytes
+    kroof, stage_k = {}, 0
+    for key, ms in kernels.items():
+        name = key.split(":", 1)[1]
+        ob = own_bytes_per_frame(name, bps, L, zoom, W, stage_k)
+        if name.startswith("xa_stage"):
+            stage_k += 1
+        ent = {"ms": ms}
+        if ob is not None and ms:
+            gbs = F * ob / (ms / 1e3) / 1e9
+            ent.update({"own_bytes": F * ob, "achieved_GBps": round(gbs, 1),
+                        "frac": round(gbs / HBM_PEAK_GBS, 4)})
+        pref = KERNEL_OF.get(name)
+        if pref and traffic_j and default_sched:
+            t = sum(v["hbm_bytes_per_step_fetch_x2"] for k2, v in traffic_j["per_kernel"].items()
+                    if k2.startswith(pref))
+            ent["traffic"] = t or None
+        if pref and sq_j and default_sched:
+            vk = [v for k2, v in sq_j["per_kernel"].items() if k2.startswith(pref)]
+            ent["valu_util"] = vk[0].get("valu_busy") if vk else None
+        kroof[key] = ent
+    dominant = max(kernels, key=lambda k: kernels[k]) if kernels else None
     out = {
-        "metric": METRIC,
+        "metric": metric_of(N, zoom),
         "value": round(value, 2),
         "unit": "MS/s",
         "n_gpus": world,
@@ -524,18 +612,23 @@ def main():
                    "f_lo_hz": f_los, "frames_per_lo": per,
                    "parallelism": f"frame-sharded x{world}, no collective (gloo barrier only)"},
         "lines_per_s": round(lines, 1),
-        "roofline": {"bound": "hbm", "kernel": dominant,
-                     "achieved": round(dom_gbs, 1) if dom_gbs else None, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(dom_gbs / HBM_PEAK_GBS, 4) if dom_gbs else None,
-                     "traffic": dom_traffic,
+        "roofline": {"bound": "hbm",
+                     "kernel": "the whole IQ -> log-PSD -> waterfall chain of a step (all launches)",
+                     "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(path_gbs / HBM_PEAK_GBS, 4),
+                     "traffic": step_traffic,
+                     "traffic_ratio": round(step_traffic / alg_step, 3) if step_traffic else None,
                      "algorithmic_bytes_per_launch": alg_step,
                      "bytes_basis": "SURVEY §8(d) per line (bps*L IQ in + 4W row + 4W ring row) x F lines "
-                                    "per launch; intermediates excluded",
-                     "avg_launch_ms": dom_ms, "valu_util": valu,
+                                    "per step; intermediates excluded",
+                     "avg_launch_ms": round(ev_ms_step, 4),
+                     "avg_launch_ms_is": "HIP-event time of one step on the launch stream (the sum of "
+                                         "the chain's launches; rocprofv3: sum of their averages)",
+                     "dominant_component": dominant,
                      "profiles": {"traffic": traffic_status, "sq": sq_status}},
-        "path_roofline": {"what": "whole IQ->log-PSD->waterfall step (all launches)",
-                          "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": round(path_gbs / HBM_PEAK_GBS, 4), "traffic": step_traffic,
+        "kernels_roofline": kroof,
+        "path_roofline": {"what": "same as roofline (the whole chain) since round 4; kept for the "
+                                  "earlier rounds' readers", "frac": round(path_gbs / HBM_PEAK_GBS, 4),
                           "event_ms_per_step": round(ev_ms_step, 4)},
         "kernels": kernels,
         "rows_finite": finite,

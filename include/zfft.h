@@ -192,19 +192,22 @@ int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *coun
 /* Comma-separated names of the intervals zfft_plan_timings returns (owned by the plan). */
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
-/* Decimator schedule: 0 = automatic (3 for batches of >= 768 frames, or >= 384 frames of
- * <= 2^19 samples -- a batched zfft_process call is judged by its whole frame count;
- * otherwise 2 for batches of >= 2^27 samples whose frames are long enough for the edge
- * windows, else 1 -- e.g. one frame per call, the reference's use; crossovers measured by
- * tools/sweep_schedule.py),
+/* Decimator schedule: 0 = automatic -- 4 for zoom 8 and frames of >= 16384 samples (every
+ * batch size); otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
+ * samples, else 2 for batches of >= 2^27 samples whose frames are long enough for the edge
+ * windows, else 1 -- e.g. one frame per call, the reference's use.  Each batch of a
+ * zfft_process call is judged by its own frame count; crossovers measured by
+ * tools/sweep_schedule.py (profiles/r04e/sweep_schedule.json).
  * 1 = blocked warm-up passes in the reference order (frames split over many waves),
  * 2 = blocked, fused commuted-order interior + exact edge windows, 3 = XA tiles (one wave per
  * frame and stage: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned;
  * each stage is one launch whose decimated output -- n_k/2 complex64 per frame -- is the next
- * stage's input in device memory).  Path 3 needs every stage array below 2^31 bytes per frame
- * (ZFFT_EUNSUPPORTED when forced beyond; auto picks a blocked path there).  All produce the
- * reference's rows within the fp32 parity gate; diagnostics / A-B only (zfft_plan.cpp
- * auto_xa, use_fused). */
+ * stage's input in device memory), 4 = PC polyphase cascade (zoom 8 only: FIRs at falling
+ * rates + the slow poles as zero-phase sections at rates 1/4 and 1/8, two launches, plus
+ * rank-~10 frame-end maps; frames >= 16384 samples, <= 65535 frames per launch).  Path 3
+ * needs every stage array below 2^31 bytes per frame; a forced path outside its domain
+ * returns ZFFT_EUNSUPPORTED.  All produce the reference's rows within the fp32 parity gate
+ * (zfft_plan.cpp auto_xa, use_fused, pc_fits). */
 int zfft_plan_path(zfft_plan *plan, int32_t path);
 
 /* Batched multi-IF (BASELINE config 4): one LO frequency per group of frames in a single
@@ -214,13 +217,6 @@ int zfft_plan_path(zfft_plan *plan, int32_t path);
  * the IFs frame by frame; n = 0 restores cfg.f_lo; n = 1 replaces cfg.f_lo.  The LO table
  * holds n rows of n_samples complex64 (n <= 256).  Waits for the plan's enqueued work. */
 int zfft_plan_set_lo_frames(zfft_plan *plan, const double *f_lo, int32_t n, int32_t frames_per_lo);
-
-/* XA schedule (path 3): decimation stages per launch.  0 = automatic (1), 1 = one launch
- * per stage (stage outputs round-trip through device memory), 2 or 3 = that many
- * consecutive stages in one launch, handing over through per-frame rings of 4096 samples
- * (32 KB per frame and fused pair; at full batches the rings outgrow L2 and the fused
- * launch is slower).  Same rows within the XA tolerance; diagnostics / A-B. */
-int zfft_plan_fuse(zfft_plan *plan, int32_t stages);
 
 /* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 16384, four-step
  * beyond), 1 = one workgroup per frame (n_fft <= 16384), 2 = four-step N1 x 256 (n_fft in

@@ -55,7 +55,7 @@ EXPORTS = [
     "zfft_decimate", "zfft_decimated_length", "zfft_waterfall_push", "zfft_waterfall_push_device",
     "zfft_waterfall_read", "zfft_waterfall_reset", "zfft_waterfall_shape", "zfft_window_values",
     "zfft_plan_tune", "zfft_plan_timing", "zfft_plan_timings", "zfft_plan_timing_names",
-    "zfft_plan_path", "zfft_plan_welch", "zfft_plan_set_lo_frames", "zfft_plan_fuse", "zfft_last_error",
+    "zfft_plan_path", "zfft_plan_welch", "zfft_plan_set_lo_frames", "zfft_last_error",
     "zfft_plan_config", "zfft_plan_row_length", "zfft_ring_create", "zfft_ring_destroy", "zfft_ring_add",
     "zfft_ring_state", "zfft_ring_take", "zfft_ring_process",
     "zfft_colormap_lut", "zfft_waterfall_colormap", "zfft_waterfall_levels",
@@ -124,7 +124,6 @@ def load(path: str = ""):
         "zfft_plan_path": (ctypes.c_int, [P, I32]),
         "zfft_plan_welch": (ctypes.c_int, [P, I32]),
         "zfft_plan_set_lo_frames": (ctypes.c_int, [P, P, I32, I32]),
-        "zfft_plan_fuse": (ctypes.c_int, [P, I32]),
         "zfft_last_error": (ctypes.c_char_p, []),
         "zfft_plan_config": (ctypes.c_int, [P, cfgp]),
         "zfft_plan_row_length": (ctypes.c_int, [P]),

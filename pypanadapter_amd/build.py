@@ -21,13 +21,14 @@ def _newest_input_mtime() -> float:
 
 
 def needs_build() -> bool:
-    """The shipped .so is missing or was built from other sources (the hash build() records
-    next to it; file times when there is no record)."""
+    """The shipped .so is missing, or was built from other sources, for another arch or with
+    build knobs (the record build() keeps next to it; file times when there is none)."""
     if not os.path.exists(LIB_PATH):
         return True
     info = build_info()
     if info.get("source_hash"):
-        return info["source_hash"] != source_hash()
+        return (info["source_hash"] != source_hash() or info.get("arch") != ARCH
+                or bool(info.get("defines")))
     return os.path.getmtime(LIB_PATH) < _newest_input_mtime()
 
 
@@ -49,8 +50,8 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH,
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
-    if out == LIB_PATH and not defines:
-        _write_build_info()
+    if out == LIB_PATH:  # a knob build there is recorded as such: the next build() replaces it
+        _write_build_info(defines)
     return out
 
 
@@ -65,13 +66,14 @@ def _git(*args):
         return None
 
 
-def _write_build_info() -> None:
-    """Next to the shipped .so (it travels with it; the GPU box has no .git): the source hash
-    and git commit it was built from, so a bench line can name both."""
+def _write_build_info(defines: tuple = ()) -> None:
+    """Next to the shipped .so (it travels with it; the GPU box has no .git): the source hash,
+    git commit, arch and build knobs it was built from, so a bench line can name them."""
     import json
     st = _git("status", "--porcelain", "--untracked-files=no")
     info = {"source_hash": source_hash(), "git_head": _git("rev-parse", "HEAD"),
-            "git_dirty": None if st is None else bool(st), "arch": ARCH}
+            "git_dirty": None if st is None else bool(st), "arch": ARCH,
+            "defines": list(defines)}
     with open(INFO_PATH, "w") as fh:
         json.dump(info, fh)
 

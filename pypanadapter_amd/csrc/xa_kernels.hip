@@ -47,31 +47,24 @@
 
 #include "zfft_device.h"
 
+// Diagnostic knobs exist only in a -DZFFT_DIAG build (tools/build_variants.py; build.py never
+// sets it): XA_STAMPS = per-phase s_memtime sums (tools/xa_stamps.py), XA_EXP = timing-only
+// knockouts with wrong results (tools/ab.sh): 1 scans, 2 state corrections, 4 LO products,
+// 8 next-tile loads, 16 output stores, 32 forward pass, 64 frame-end tiles as fast tiles.
+// The production variants measured against the alternatives are DESIGN.md §3.1's.
+#if defined(ZFFT_DIAG) && ZFFT_DIAG
 #ifndef XA_STAMPS
 #define XA_STAMPS 0
 #endif
-#ifndef XA_WPS
-#define XA_WPS 2  // waves per SIMD the register budget is cut for
-#endif
 #ifndef XA_EXP
-#define XA_EXP 0  // timing-only knockouts (wrong results; tools/ab.sh A/B): 1 scans, 2 state
-                  // corrections, 4 LO products, 8 next-tile loads, 16 output stores, 32 forward pass,
-                  // 64 frame-end tiles loaded as fast tiles
+#define XA_EXP 0
 #endif
-#ifndef XA_PIN
-#define XA_PIN 0  // the FIR neighbour share P accumulated inside the forward pass (v dies at once)
+#else
+#if defined(XA_STAMPS) || defined(XA_EXP)
+#error "XA_STAMPS / XA_EXP are diagnostic knobs: build with -DZFFT_DIAG"
 #endif
-#ifndef XA_NT
-#define XA_NT 3   // cache policy: 1 = nt (streaming) tile loads, 2 = nt output stores
-#endif
-#ifndef XA_DEFER
-#define XA_DEFER 0  // 1: an inside tile's output stores issued after the next tile's input wait
-#endif
-#ifndef XA_PF
-#define XA_PF 0   // next-tile load issue points: 0 = 4 groups at the tile start, 2 after the
-                  // forward pass, 2 after the scan; 1 = all 8 after the forward pass;
-                  // 2 = no prefetch: a tile's loads at its own start; 4 = all 8 at the tile
-                  // start; 5 = groups 0-3 after the flush, 4-7 at the next tile's start
+#define XA_STAMPS 0
+#define XA_EXP 0
 #endif
 
 namespace zfft {
@@ -81,10 +74,6 @@ namespace xa {
 // once: one LDS round trip per direction and tile (two halves in turn: 4 % slower at cfg2).
 // 4-wave workgroups: 2 of them (78 KB of LDS each) fill a CU at 2 waves per SIMD.
 constexpr int kHalfRows = 32;           // rows of one transpose half (32 lanes' sub-blocks)
-#ifndef XA_HALVES
-#define XA_HALVES 2
-#endif
-constexpr int kHalves = XA_HALVES;      // input-transpose halves held in LDS at once (1: in turn)
 constexpr int kWaves = 4;               // waves (frames) per workgroup
 constexpr int kLagChunks = kXaLag / 64; // held output chunks of a tile
 
@@ -104,10 +93,10 @@ struct Geo {
   // LDS per wave: the tile transpose (both halves) + FIR carry (12 used) + frame-end v
   // carry (the 64 v before the last tile)
   // (the output transpose, 64 rows of kHeldRow, reuses the input transpose's space)
-  static constexpr int kIn = kHalves == 2 ? 2 * kHalfRows * kRow : 64 * (B / 2 + 2);
+  static constexpr int kIn = 2 * kHalfRows * kRow;
   static constexpr int kMain = kIn > 64 * kHeldRow ? kIn : 64 * kHeldRow;
   static constexpr int kBuf = kMain + 16 + 64;
-  static constexpr int kWavesPerSimd = B == 32 ? XA_WPS : 1;  // the register budget is cut for
+  static constexpr int kWavesPerSimd = B == 32 ? 2 : 1;  // the register budget is cut for
 };
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -148,8 +137,8 @@ template <int DT> struct Pair {
 };
 
 // one raw element (or pair) through a buffer resource (out-of-range offsets read 0)
-constexpr int kLoadAux = (XA_NT & 1) ? 2 : 0;   // aux 2 = nt
-constexpr int kStoreAux = (XA_NT & 2) ? 2 : 0;
+constexpr int kLoadAux = 2;   // aux 2 = nt (streaming): tile loads and output stores
+constexpr int kStoreAux = 2;
 template <class T>
 __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   T v;
@@ -434,32 +423,6 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
   v2f held[kLagChunks];
 #pragma unroll
   for (int c = 0; c < kLagChunks; ++c) held[c] = splat(0.f);
-  // XA_DEFER: an inside tile's stores wait in registers until the next tile has consumed its
-  // prefetched input.  vmcnt counts loads and stores in issue order, and the compiler's wait
-  // for the last prefetched chunk at the tile start is vmcnt(0): stores issued at the end of
-  // a tile would be waited for there; issued after that wait and before the next tile's loads
-  // they are long complete by the time those loads are waited for.
-  constexpr int nwD = (kChunks - kLagChunks) / 2, ncD = kChunks - kLagChunks - 2 * nwD;
-  v4f dw[nwD > 0 ? nwD : 1];
-  v2f dc[ncD > 0 ? ncD : 1], dh[kLagChunks];
-  int d_tile = -1, d_held = -1;  // tile of the pending flush / of the pending held outputs
-  auto issue_deferred = [&](int ln) {
-    if (d_held >= 0) {
-      const int m0 = m_of(d_held, (kChunks - kLagChunks) * 64 + ln);
-#pragma unroll
-      for (int c = 0; c < kLagChunks; ++c) st_out(o + m0 + 64 * c, dh[c]);
-      d_held = -1;
-    }
-    if (d_tile >= 0) {
-#pragma unroll
-      for (int c = 0; c < nwD; ++c)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, dw[c]), orsrc,
-                                               (uint32_t)(m_of(d_tile, 128 * c + 2 * ln) * 8), 0, kStoreAux);
-#pragma unroll
-      for (int c = 0; c < ncD; ++c) st_out(o + m_of(d_tile, ln) + 64 * (2 * nwD + c), dc[c]);
-      d_tile = -1;
-    }
-  };
   auto flush_tile = [&](int tile, const v2f *h, int ln) {
     const int m0 = m_of(tile, ln);
     v2f *__restrict__ od = o + m0;
@@ -487,12 +450,6 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       for (int c = 2 * nw; c < kChunks; ++c) vc[c] = hr[c * (64 / K) * kHeldRow];
       if (inside && (XA_EXP & 16)) {
         if (vw[0].x == 1.2345f && vc[kChunks - 1].x == 1.2345f) od[0] = vc[kChunks - 1];
-      } else if (inside && XA_DEFER) {
-#pragma unroll
-        for (int c = 0; c < nw; ++c) dw[c] = vw[c];
-#pragma unroll
-        for (int c = 2 * nw; c < kChunks - kLagChunks; ++c) dc[c - 2 * nw] = vc[c];
-        d_tile = tile;
       } else if (inside) {
 #pragma unroll
         for (int c = 0; c < nw; ++c)
@@ -536,11 +493,7 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     }
     // wave-uniform: every held output of the tile inside the frame -> unconditional stores
     const bool inside = m_of(tile, (kChunks - kLagChunks) * 64) >= 0 && m_of(tile, kChunks * 64) <= n_out;
-    if (inside && XA_DEFER && q != nullptr) {
-#pragma unroll
-      for (int c = 0; c < kLagChunks; ++c) dh[c] = held[c];
-      d_held = tile;
-    } else if (inside) {
+    if (inside) {
 #pragma unroll
       for (int c = 0; c < kLagChunks; ++c) st_out(o + m0 + 64 * c, held[c]);
     } else {
@@ -608,14 +561,6 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     }
     const int base = tau * T;
     const bool last = tau == nt - 1;
-    if (XA_PF == 2) {  // this tile's loads at its start (no register prefetch across tiles)
-#pragma unroll
-      for (int g = 0; g < 8; ++g) issue_group(g);
-    }
-    if (XA_PF == 5) {  // the second half of this tile's loads (the first came with the last flush)
-#pragma unroll
-      for (int g = 4; g < 8; ++g) issue_group(g);
-    }
     v2f y[B];
     {
       const bool fast = fast_tile(base);  // wave-uniform
@@ -633,21 +578,6 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
         }
         __builtin_amdgcn_wave_barrier();
       };
-      // kHalves == 1: the tile goes through LDS as two column halves in turn (columns
-      // 16 hf .. 16 hf + 15 of all 64 rows, row stride kRowH): every lane takes 16 of its
-      // samples per half, so no lane's registers are written under a divergent mask
-      constexpr int kRowH = B / 2 + 2;  // 144-B rows: b128 reads conflict-free per 16 lanes
-      auto read_col_half = [&](int hf) {
-        __builtin_amdgcn_wave_barrier();
-        const LP4 rp = (LP4)(buf + ln * kRowH);
-#pragma unroll
-        for (int t = 0; t < B / 4; ++t) {
-          const v4f w = rp[t];
-          y[hf * (B / 2) + 2 * t] = v2f{w.x, w.y};
-          y[hf * (B / 2) + 2 * t + 1] = v2f{w.z, w.w};
-        }
-        __builtin_amdgcn_wave_barrier();
-      };
       auto fast_chunk = [&](int q) -> v4f {
         // FLIP: the pair was read from descending addresses, so its halves swap
         v2f x0 = cvt_raw<DT>(FLIP ? pf[q].b : pf[q].a), x1 = cvt_raw<DT>(FLIP ? pf[q].a : pf[q].b);
@@ -660,51 +590,21 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
       };
       if (fast) {
         // sample s at row s/B, col s%B; chunk q's pair of lane l is row 4q + l/16, cols
-        // 2 (l%16) + {0, 1}: one b128
-        if constexpr (kHalves == 2) {  // the 64 rows contiguous (both halves at once)
-          const LP4 st2 = (LP4)(buf + (ln / 16) * kRow + 2 * (ln % 16));
+        // 2 (l%16) + {0, 1}: one b128; the 64 rows contiguous (both halves at once)
+        const LP4 st2 = (LP4)(buf + (ln / 16) * kRow + 2 * (ln % 16));
 #pragma unroll
-          for (int q = 0; q < kCh; ++q) st2[q * (4 * kRow / 2)] = fast_chunk(q);
-          read_all_rows();
-        } else {
-          v4f cx[kCh];
-#pragma unroll
-          for (int q = 0; q < kCh; ++q) cx[q] = fast_chunk(q);
-          // lane l's pair sits in column half (l % 16) / 8, at column 2 (l % 8)
-          const LP4 st2 = (LP4)(buf + (ln / 16) * kRowH + 2 * (ln % 8));
-#pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
-            if (((ln >> 3) & 1) == hf) {
-#pragma unroll
-              for (int q = 0; q < kCh; ++q) st2[q * (4 * kRowH / 2)] = cx[q];
-            }
-            read_col_half(hf);
-          }
-        }
+        for (int q = 0; q < kCh; ++q) st2[q * (4 * kRow / 2)] = fast_chunk(q);
+        read_all_rows();
       } else {
-        if constexpr (kHalves == 2) {
 #pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
+        for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll 4
-            for (int qq = 0; qq < B / 2; ++qq)
-              st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = ext(base + ln + 64 * (hf * (B / 2) + qq));
-          }
-          read_all_rows();
-        } else {
-          // sample 64 Q + ln: row 2 Q + ln / 32, column ln % 32, in column half (ln % 32) / 16
-          const LP sth = buf + (ln / 32) * kRowH + (ln % 16);
-#pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
-            if (((ln >> 4) & 1) == hf) {
-#pragma unroll 4
-              for (int Q = 0; Q < B; ++Q) sth[2 * Q * kRowH] = ext(base + ln + 64 * Q);
-            }
-            read_col_half(hf);
-          }
+          for (int qq = 0; qq < B / 2; ++qq)
+            st[hf * kHalfRows * kRow + G::kRowsPerChunk * kRow * qq] = ext(base + ln + 64 * (hf * (B / 2) + qq));
         }
+        read_all_rows();
       }
     }
-    if (XA_DEFER) issue_deferred(ln);
     next_fast = tau + 1 < nt && fast_tile(base + T);  // wave-uniform
     next_i0 = base + T - kPad;
     {  // (FLIP: the pair's elements i0, i0 + 1 sit at len-1-i0 and len-2-i0)
@@ -714,18 +614,10 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     // the next tile's loads: groups 0-3 now, 4-5 after the forward pass, 6-7 after the scan
     // (later issue points leave the register allocator room it does not use: spills; all
     // eight groups at the tile start measured no faster)
-    if (XA_PF == 0 || XA_PF == 4) {
-      issue_group(0);
-      issue_group(1);
-      issue_group(2);
-      issue_group(3);
-    }
-    if (XA_PF == 4) {  // all eight groups at the tile start
-      issue_group(4);
-      issue_group(5);
-      issue_group(6);
-      issue_group(7);
-    }
+    issue_group(0);
+    issue_group(1);
+    issue_group(2);
+    issue_group(3);
     XA_STAMP(0);
 
     // ---- forward all-pole cascade: one pass from a zero state streaming the FIR (v0 -> h
@@ -760,11 +652,10 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
           for (int t = 0; t < 25; ++t) m25s[t] = tbs->m25[t];
           // frame end: the 64 v before the last tile (lanes 64 - 64/B .. 63 of the tile
           // before it) and the last tile's two lanes around e-25 .. e-1 go to LDS for
-          // f = N v -- v0 during the pass, the entering state's part once it is known.  Those
-          // two tiles run a copy of the pass with the stores; every other tile's pass lets
-          // each v die as soon as it has entered the FIR (own outputs h, neighbour share P).
+          // f = N v -- v0 after the pass (v overwrites y in place), the entering state's part
+          // once it is known.  The neighbour share P is accumulated from the last 23 v after
+          // the pass (accumulating it inside the pass measured no faster).
           {
-            constexpr bool kStore = true;
             LP wrow = buf;
             bool wlane = false;
             if (tau >= nt - 2) {
@@ -786,51 +677,29 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
                 const int tap = 24 + t - 1 - 2 * k;
                 if (tap >= 0 && tap < 25) h[k] = vfma(splat(m25s[tap]), v, h[k]);
               }
-              // this lane's share of its right neighbour's outputs: W[m] = v[B - 24 + m],
-              // 1 <= m < 24
+              y[t] = v;
+            }
+            // this lane's share of its right neighbour's outputs: W[m] = v[B - 24 + m],
+            // 1 <= m < 24
+#pragma unroll
+            for (int t = B - 23; t < B; ++t) {
 #pragma unroll
               for (int k = 0; k < 12; ++k) {
                 const int tap = t - (B - 24) - 1 - 2 * k;
-                if (XA_PIN && t >= B - 23 && tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), v, P[k]);
-              }
-              if (!XA_PIN) y[t] = v;
-              if constexpr (kStore) {
-                if (XA_PIN && wlane) wrow[t] = v;
+                if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), y[t], P[k]);
               }
             }
-            if (!XA_PIN) {
+            if (wlane) {
+              LP4 wp = (LP4)wrow;
 #pragma unroll
-              for (int t = B - 23; t < B; ++t) {
-#pragma unroll
-                for (int k = 0; k < 12; ++k) {
-                  const int tap = t - (B - 24) - 1 - 2 * k;
-                  if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), y[t], P[k]);
-                }
-              }
-              if (wlane) {
-                LP4 wp = (LP4)wrow;
-#pragma unroll
-                for (int t = 0; t < B / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
-              }
+              for (int t = 0; t < B / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
             }
           }
           to_modal<0>(tab, s, m);
         }
         XA_STAMP(1);
-        if (XA_PF == 1) {
-          issue_group(0);
-          issue_group(1);
-          issue_group(2);
-          issue_group(3);
-        }
-        if (XA_PF != 4 && XA_PF != 5 && XA_PF != 2) {
-          issue_group(4);
-          issue_group(5);
-        }
-        if (XA_PF == 1) {
-          issue_group(6);
-          issue_group(7);
-        }
+        issue_group(4);
+        issue_group(5);
         fold_entering<0>(m, m_in, tab, ln == 0);
         modal_scan<B, 0, true>(m, tab, ln, xw_l[0][ln & 15]);
 #pragma unroll
@@ -839,10 +708,8 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
         for (int r = 0; r < 8; ++r) m_in.r[r] = lane_of(m.r[r], 63);  // next tile's entering state
       }
       XA_STAMP(2);
-      if (XA_PF == 0) {
-        issue_group(6);
-        issue_group(7);
-      }
+      issue_group(6);
+      issue_group(7);
       // + the entering state's response through the FIR (own outputs, neighbour share);
       // row k's constants are read once output k-4 is done (at most 4 rows in flight)
       // (scalar reads; row k once output k-4 is done: LDS broadcast reads measured 6 % slower)
@@ -980,13 +847,8 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     }
     XA_STAMP(8);
     flush_tile(tau, h, ln);
-    if (XA_PF == 5) {  // half of the next tile's loads: 32 VGPRs across the tile boundary
-#pragma unroll
-      for (int g = 0; g < 4; ++g) issue_group(g);
-    }
     XA_STAMP(9);
   }
-  if (XA_DEFER) issue_deferred(lane);
   finish_held(nt - 1, nullptr, nullptr, lane);  // the last tile's top state was exact
 #if XA_STAMPS
   if (lane == 0) {
@@ -995,516 +857,6 @@ __global__ __launch_bounds__(64 * kWaves, Geo<B>::kWavesPerSimd) void xa_stage_k
     atomicAdd(&g_xa_stamps[kStampSegs], (unsigned long long)nt);
   }
 #endif
-}
-
-// ---------------------------------------------------------------------------------------
-// Fused stages: D <= 3 consecutive decimation stages of one frame in one wave.  Stage s
-// hands its output to stage s+1 through a per-frame ring of kRing complex64 in global
-// memory (sample i at slot (i + 27) % kRing: a stage's tiles then start on a 2048-aligned
-// slot), so the intermediate never makes a round trip through HBM beyond what the caches
-// evict; the last stage writes the natural output row.  A wave-uniform schedule runs the
-// deepest stage whose next tile's inputs are final (stage s has finalised outputs m <=
-// 1024 (tiles - 1) + 810: the top kXaLag outputs of its latest tile wait for the next), which
-// also keeps every stage within kRing of its consumer.  One copy of the tile body serves
-// every stage (s at run time): stage 0 reads the frame (LO mix, in_dtype, flip, register
-// prefetch of its next tile), later stages read the ring at their tile start.  Per-stage
-// carries (modal state, FIR share, frame-end v, held outputs) live in LDS between tiles.
-constexpr int kRing = 4096;
-struct XaFuseArgs {
-  int D;        // stages in this launch (1..3)
-  int n[3];     // their input lengths
-  v2f *ring;    // [frames][D - 1][kRing]
-};
-struct StageLds {
-  v2f m_in[8];                // forward modal state entering the stage's next tile (uniform)
-  v2f pcarry[16];             // lane 63's FIR share for the next tile's lane 0 (12 used)
-  v2f vcarry[64];             // the 64 v before the last tile
-  v2f held[kLagChunks][64];   // top kXaLag outputs of the latest tile, lane-major
-};
-
-template <bool MIX, int DT, int FLIP>
-__global__ __launch_bounds__(64 * kWaves, 2) void xa_fused_kernel(
-    InDesc in, XaFuseArgs a, const v2f *__restrict__ lo, v2f *__restrict__ out, int frames,
-    const XaTab *tab_g) {
-  constexpr int B = 32;
-  using G = Geo<B>;
-  constexpr int K = G::K, T = G::T, kRow = G::kRow, kHeldRow = G::kHeldRow, kChunks = G::kOutChunks;
-  constexpr int kRowH = B / 2 + 2;              // column-half transpose rows (144 B)
-  constexpr int kMainF = 64 * (B / 2 + 2);      // = 64 kRowH: either transpose
-  static_assert(64 * kRowH == kMainF && 4 * kRow <= kMainF, "LDS geometry");
-  __shared__ __attribute__((aligned(16))) v2f lds_all[kWaves][kMainF];
-  __shared__ __attribute__((aligned(16))) StageLds sl_all[kWaves][3];
-  const CT tab = (CT)tab_g;
-  __shared__ __attribute__((aligned(16))) v4f lag_l[kXaLag * 2];  // two planes, as above
-  for (int i = threadIdx.x; i < kXaLag * 2; i += 64 * kWaves)
-    lag_l[(i & 1) * kXaLag + (i >> 1)] = ((const v4f *)tab_g->lag)[i];
-  __shared__ v4f xw_l[2][16];
-  if (threadIdx.x < 32) xw_l[threadIdx.x >> 4][threadIdx.x & 15] = ((const v4f *)((threadIdx.x >> 4) ? tab_g->b.xr : tab_g->f.xr))[threadIdx.x & 15];
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int f = blockIdx.x * kWaves + wv;
-  if (f >= frames) return;  // whole wave
-  if constexpr (MIX) lo = lo_row(lo, in, f);
-  const LP buf0 = (LP)lds_all[wv];
-  const int D = a.D;
-
-  // ---- stage 0 reader: the caller's frame (as xa_stage_kernel) ----
-  typedef typename Raw<DT>::T RawT;
-  const RawT *__restrict__ src = (const RawT *)in.p + (int64_t)f * in.stride;
-  const int n0 = a.n[0];
-  auto X0 = [&](int i) -> v2f {
-    v2f v = load_in_t<DT, FLIP>(in, f, i);
-    if constexpr (MIX) v = cmul(v, lo[i]);
-    return v;
-  };
-  constexpr int kPer = 2, kCh = B / kPer, kSpan = 64 * kPer;
-  typedef Pair<DT> LoadT;
-  v2f wl0 = splat(0.f), wl1 = splat(0.f);
-  if constexpr (MIX) {
-    wl0 = lo[min(kPer * lane, n0 - 1)] * 0.70710678118654752f;
-    wl1 = lo[min(kPer * lane + 1, n0 - 1)] * 0.70710678118654752f;
-  }
-  v2f cqv = splat(0.f);
-  LoadT pf[kCh];
-  bool next_fast = false;
-  int next_i0 = 0;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)src, (short)0, (int)(in.len * (int64_t)sizeof(RawT)), 0x00020000);
-  uint32_t next_off = 0;
-  auto issue_group = [&](int g) {
-    if (MIX && g == 0 && next_fast) cqv = lo[next_i0 + kSpan * (lane % kCh)];
-#pragma unroll
-    for (int q = g * (kCh / 8); q < (g + 1) * (kCh / 8); ++q)
-      pf[q] = buf_load<LoadT>(rsrc, next_off + (uint32_t)((FLIP ? -kSpan : kSpan) * q * (int)sizeof(RawT)));
-  };
-  // ---- rings: stage s < D - 1 writes ring s, stage s > 0 reads ring s - 1 ----
-  v2f *__restrict__ rings = a.ring + (int64_t)f * (D > 1 ? D - 1 : 0) * kRing;
-  const __amdgpu_buffer_rsrc_t ring_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)rings, (short)0, (D > 1 ? D - 1 : 1) * kRing * 8, 0x00020000);
-  const int nL = a.n[D - 1], nL_out = (nL + 1) >> 1;
-  v2f *__restrict__ o_last = out + (int64_t)f * nL_out;
-  const __amdgpu_buffer_rsrc_t orsrc_last =
-      __builtin_amdgcn_make_buffer_rsrc((void *)o_last, (short)0, nL_out * 8, 0x00020000);
-
-  auto n_of = [&](int s) { return s == 0 ? a.n[0] : s == 1 ? a.n[1] : a.n[2]; };
-  auto nt_of = [&](int s) { return (n_of(s) + 2 * kPad + 15) / T + 1; };
-  int cnt0 = 0, cnt1 = 0, cnt2 = 0;  // tiles done per stage (wave-uniform)
-  auto cnt_of = [&](int s) { return s == 0 ? cnt0 : s == 1 ? cnt1 : cnt2; };
-  // stage s's inputs final up to index `need`: stage s-1 done, or its finalised outputs
-  auto ready = [&](int s) {
-    const int tau = cnt_of(s), n = n_of(s);
-    if (tau >= nt_of(s)) return false;
-    const int c = cnt_of(s - 1);
-    if (c >= nt_of(s - 1)) return true;
-    const int need = tau * T + (T - 1) >= n + kPad ? n - 1 : tau * T + T - 1 - kPad;
-    return c > 0 && (c - 1) * (T / 2) + (T / 2 - kXaLag - (kPad + 15) / 2 - 1) >= need;
-  };
-
-  while (true) {
-    int s = D - 1;
-    while (s > 0 && !ready(s)) --s;
-    s = __builtin_amdgcn_readfirstlane(s);
-    const int tau = cnt_of(s);
-    const int n = n_of(s), e = n + 2 * kPad, n_out = (n + 1) >> 1, nt = nt_of(s);
-    const bool is_last_stage = s == D - 1;
-    StageLds *sl = &sl_all[wv][s];
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    LP buf = buf0;
-    {
-      LP b = buf0;
-      asm volatile("" : "+s"(b));
-      buf = b;
-    }
-    LP pcarry = (LP)sl->pcarry, vcarry = (LP)sl->vcarry;
-    // this stage's reader.  Ring data were stored by this wave in earlier iterations: wait
-    // until every store has completed (vmcnt counts stores too), and read with nt, served by
-    // L2 (never a stale L1 line of an earlier pass over the same slots)
-    if (s > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    auto X = [&](int i) -> v2f {
-      if (s == 0) return X0(i);
-      return __builtin_nontemporal_load(rings + (int64_t)(s - 1) * kRing + ((i + kPad) & (kRing - 1)));
-    };
-    auto ext = [&](int j) -> v2f {
-      if (j < kPad) return 2.f * X(0) - X(kPad - j);
-      if (j < n + kPad) return X(j - kPad);
-      if (j < e) return 2.f * X(n - 1) - X(2 * n + kPad - 2 - j);
-      return splat(0.f);
-    };
-    // this stage's writer: ring slot or natural row position of output m
-    auto woff = [&](int m) -> int { return is_last_stage ? m : (s * kRing + ((m + kPad) & (kRing - 1))); };
-    v2f *__restrict__ o = is_last_stage ? o_last : rings;
-    const __amdgpu_buffer_rsrc_t orsrc = is_last_stage ? orsrc_last : ring_rsrc;
-    auto m_of = [&](int tile, int idx) { return tile * (T / 2) - (kPad + 15) / 2 + idx; };
-
-    if (tau == 0) {  // stage start: forward pre-history of constant ext[0]
-      const v2f x0 = v2f{uni(ext(0).x), uni(ext(0).y)};
-      if (ln < 8) sl->m_in[ln] = tab->f.ss[ln] * x0;
-      const v2f vs = tab->vss * x0;
-      if (ln < 12) {
-        CT tb = fresh(tab);
-        v2f acc = splat(0.f);
-        for (int t = 0; t < 25; ++t)
-          if (2 * ln + t + 1 < 24) acc = vfma(splat(tb->m25[t]), vs, acc);
-        pcarry[ln] = acc;
-      }
-      vcarry[ln] = vs;
-      __builtin_amdgcn_wave_barrier();
-    }
-    const int base = tau * T;
-    const bool last = tau == nt - 1;
-    auto fast_tile = [&](int b) { return b >= kPad && b + T <= n + kPad; };
-    v2f y[B];
-    {
-      const bool fast = fast_tile(base);
-      auto read_col_half = [&](int hf) {
-        __builtin_amdgcn_wave_barrier();
-        const LP4 rp = (LP4)(buf + ln * kRowH);
-#pragma unroll
-        for (int t = 0; t < B / 4; ++t) {
-          const v4f w = rp[t];
-          y[hf * (B / 2) + 2 * t] = v2f{w.x, w.y};
-          y[hf * (B / 2) + 2 * t + 1] = v2f{w.z, w.w};
-        }
-        __builtin_amdgcn_wave_barrier();
-      };
-      if (fast) {
-        v4f cx[kCh];
-        if (s == 0) {
-#pragma unroll
-          for (int q = 0; q < kCh; ++q) {
-            v2f x0 = cvt_raw<DT>(FLIP ? pf[q].b : pf[q].a), x1 = cvt_raw<DT>(FLIP ? pf[q].a : pf[q].b);
-            if constexpr (MIX) {
-              const v2f c = lane_of(cqv, q);
-              x0 = cmul2(x0, cmul2(c, wl0));
-              x1 = cmul2(x1, cmul2(c, wl1));
-            }
-            cx[q] = v4f{x0.x, x0.y, x1.x, x1.y};
-          }
-        } else {  // ring s - 1: samples base - 27 + 128 q + 2 ln + {0, 1} at slots base % kRing + ...
-          const uint32_t off0 = (uint32_t)(((s - 1) * kRing + (base & (kRing - 1)) + 2 * ln) * 8);
-#pragma unroll
-          for (int q = 0; q < kCh; ++q)
-            cx[q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, off0 + (uint32_t)(q * kSpan * 8), 0, 2));
-        }
-        const LP4 st2 = (LP4)(buf + (ln / 16) * kRowH + 2 * (ln % 8));
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          if (((ln >> 3) & 1) == hf) {
-#pragma unroll
-            for (int q = 0; q < kCh; ++q) st2[q * (4 * kRowH / 2)] = cx[q];
-          }
-          read_col_half(hf);
-        }
-      } else {
-        const LP sth = buf + (ln / 32) * kRowH + (ln % 16);
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          if (((ln >> 4) & 1) == hf) {
-#pragma unroll 4
-            for (int Q = 0; Q < B; ++Q) sth[2 * Q * kRowH] = ext(base + ln + 64 * Q);
-          }
-          read_col_half(hf);
-        }
-      }
-    }
-    if (s == 0) {  // stage 0's next tile: register prefetch
-      next_fast = tau + 1 < nt && fast_tile(base + T);
-      next_i0 = base + T - kPad;
-      const int i0 = base + T - kPad + kPer * ln;
-      next_off = (uint32_t)((FLIP ? in.len - kPer - i0 : (int64_t)i0) * (int64_t)sizeof(RawT));
-      issue_group(0);
-      issue_group(1);
-      issue_group(2);
-      issue_group(3);
-    }
-
-    v2f h[K];
-    Md me;
-    {
-      v2f P[12];
-#pragma unroll
-      for (int k = 0; k < K; ++k) h[k] = splat(0.f);
-#pragma unroll
-      for (int k = 0; k < 12; ++k) P[k] = splat(0.f);
-      {
-        Md m;
-        {
-          float a1[4], a2[4];
-          v2f st[8];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) st[r] = splat(0.f);
-          const CT tbs = fresh(tab);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            a1[k] = tbs->f.a1[k];
-            a2[k] = tbs->f.a2[k];
-          }
-          float m25s[25];
-#pragma unroll
-          for (int t = 0; t < 25; ++t) m25s[t] = tbs->m25[t];
-#pragma unroll
-          for (int t = 0; t < B; ++t) {
-            const v2f v = ap_step(y[t], st, a1, a2);
-            y[t] = v;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-              const int tap = 24 + t - 1 - 2 * k;
-              if (tap >= 0 && tap < 25) h[k] = vfma(splat(m25s[tap]), v, h[k]);
-            }
-          }
-          to_modal<0>(tab, st, m);
-#pragma unroll
-          for (int t = B - 23; t < B; ++t) {
-#pragma unroll
-            for (int k = 0; k < 12; ++k) {
-              const int tap = t - (B - 24) - 1 - 2 * k;
-              if (tap >= 0 && tap < 25) P[k] = vfma(splat(m25s[tap]), y[t], P[k]);
-            }
-          }
-          if (tau >= nt - 2) {
-            const int la = max(0, (e - 25 - base) / B);
-            if ((!last && ln >= 64 - 64 / B) || (last && (ln == la || ln == la + 1))) {
-              LP4 wp = (LP4)(last ? buf + (ln - la) * kRow : vcarry + (ln - (64 - 64 / B)) * B);
-#pragma unroll
-              for (int t = 0; t < B / 2; ++t) wp[t] = v4f{y[2 * t].x, y[2 * t].y, y[2 * t + 1].x, y[2 * t + 1].y};
-            }
-          }
-        }
-        if (s == 0) {
-          issue_group(4);
-          issue_group(5);
-        }
-        Md m_in;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) m_in.r[r] = sl->m_in[r];  // (uniform broadcast reads)
-        fold_entering<0>(m, m_in, tab, ln == 0);
-        modal_scan<B, 0, true>(m, tab, ln, xw_l[0][ln & 15]);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) me.r[r] = wave_shift<kShr1>(m_in.r[r], m.r[r]);
-        __builtin_amdgcn_wave_barrier();
-        if (ln == 63) {
-#pragma unroll
-          for (int r = 0; r < 8; ++r) sl->m_in[r] = m.r[r];  // the next tile's entering state
-        }
-      }
-      if (s == 0) {
-        issue_group(6);
-        issue_group(7);
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const CT t = k >= 4 ? after(tab, h[k - 4]) : fresh(tab);
-        h[k] = add_modal(h[k], t->gown[k], me);
-      }
-#pragma unroll
-      for (int k = 0; k < 12; ++k) {
-        const CT t = after(tab, k >= 4 ? P[k - 4] : h[K - 4 + k]);
-        P[k] = add_modal(P[k], t->gnb[k], me);
-      }
-      {
-        const LP4 pc = (LP4)pcarry;
-#pragma unroll
-        for (int k2 = 0; k2 < 6; ++k2) {
-          const v4f c4 = pc[k2];
-          h[2 * k2] += wave_shift<kShr1>(v2f{c4.x, c4.y}, P[2 * k2]);
-          h[2 * k2 + 1] += wave_shift<kShr1>(v2f{c4.z, c4.w}, P[2 * k2 + 1]);
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (ln == 63) {
-          LP4 pw = (LP4)pcarry;
-#pragma unroll
-          for (int k2 = 0; k2 < 6; ++k2) pw[k2] = v4f{P[2 * k2].x, P[2 * k2].y, P[2 * k2 + 1].x, P[2 * k2 + 1].y};
-        }
-      }
-    }
-    const int la = max(0, (e - 25 - base) / B);
-    if (tau >= nt - 2 && ((!last && ln >= 64 - 64 / B) || (last && (ln == la || ln == la + 1)))) {
-      LP wp = last ? buf + (ln - la) * kRow : vcarry + (ln - (64 - 64 / B)) * B;
-#pragma unroll 4
-      for (int t = 0; t < B; ++t) {
-        CT tb = fresh(tab);
-        v2f acc = wp[t];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) acc = vfma(splat(tb->fcat[t][r]), me.r[r], acc);
-        wp[t] = acc;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    v2f h_ss = splat(0.f);
-    if (last) {
-      auto v_at = [&](int p) -> v2f {
-        const int r = p - base;
-        return r < 0 ? vcarry[64 + r] : buf[(r / B - la) * kRow + (r % B)];
-      };
-      LP fbuf = buf + 2 * kRow, tbuf = buf + 3 * kRow;
-      if (ln < 16) {
-        CT tb = fresh(tab);
-        v2f acc = splat(0.f);
-        for (int i = 0; i < 9; ++i) acc = vfma(splat(tb->n9[i]), v_at(e - 16 + ln - i), acc);
-        fbuf[ln] = acc;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const v2f fe = fbuf[15];
-      h_ss = fe * fresh(tab)->mp_sum;
-      const int j0 = (e - 16) | 1;
-      if (ln < 8 && j0 + 2 * ln <= e - 1) {
-        CT tb = fresh(tab);
-        const int j = j0 + 2 * ln;
-        v2f acc = splat(0.f);
-        for (int t = 0; t < 17; ++t) {
-          const int sidx = j + t - (e - 16);
-          acc = vfma(splat(tb->mp17[t]), sidx < 16 ? fbuf[sidx] : fe, acc);
-        }
-        tbuf[ln] = acc;
-      }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int j = base + B * ln - 15 + 2 * k;
-        if (j > e - 1) h[k] = h_ss;
-        else if (j > e - 17) h[k] = tbuf[(j - j0) >> 1];
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-
-    Md q_exit;
-    {
-      Md qe;
-      {
-        Md m;
-        {
-          float a1[4], a2[4];
-          load_ap<1>(tab, a1, a2);
-          v2f st[8];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) st[r] = splat(0.f);
-#pragma unroll
-          for (int k = K - 1; k >= 0; --k) h[k] = ap_step(h[k], st, a1, a2);
-          to_modal<1>(tab, st, m);
-        }
-        Md qtop;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) qtop.r[r] = splat(0.f);
-        if (last) {
-          CT tb = fresh(tab);
-#pragma unroll
-          for (int r = 0; r < 8; ++r) qtop.r[r] = tb->b.ss[r] * h_ss;
-          fold_entering<1>(m, qtop, tab, ln == 63);
-        }
-        modal_scan<B, 1, false>(m, tab, ln, xw_l[1][ln & 15]);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) qe.r[r] = wave_shift<kShl1>(qtop.r[r], m.r[r]);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) q_exit.r[r] = lane_of(m.r[r], 0);
-      }
-#pragma unroll
-      for (int k = K - 1; k >= 0; --k) {
-        const CT t = k < K - 4 ? after(tab, h[k + 4]) : fresh(tab);
-        h[k] = add_modal(h[k], t->lag[K - 1 - k], qe);
-      }
-    }
-    // held outputs of this stage's previous tile (+ C A2^d T q), then this tile's outputs
-    auto store_held = [&](int tile, const Md *q) {
-      const int m0 = m_of(tile, (kChunks - kLagChunks) * 64 + ln);
-      v2f hv[kLagChunks];
-#pragma unroll
-      for (int c = 0; c < kLagChunks; ++c) {
-        v2f v = ((LP)sl->held[c])[ln];
-        if (q != nullptr) {
-          const int d = kXaLag - 1 - 64 * c - ln;
-          const v4f l0 = lag_l[d], l1 = lag_l[kXaLag + d];
-          v = vfma(splat(l0.x), q->r[0], v);
-          v = vfma(splat(l0.y), q->r[1], v);
-          v = vfma(splat(l0.z), q->r[2], v);
-          v = vfma(splat(l0.w), q->r[3], v);
-          v = vfma(splat(l1.x), q->r[4], v);
-          v = vfma(splat(l1.y), q->r[5], v);
-          v = vfma(splat(l1.z), q->r[6], v);
-          v = vfma(splat(l1.w), q->r[7], v);
-        }
-        hv[c] = v;
-      }
-#pragma unroll
-      for (int c = 0; c < kLagChunks; ++c) {
-        const int m = m0 + 64 * c;
-        if (m >= 0 && m < n_out) st_out(o + woff(m), hv[c]);
-      }
-    };
-    if (tau > 0) store_held(tau - 1, &q_exit);
-    {
-      const int m0 = m_of(tau, ln);
-      const bool inside = m_of(tau, 0) >= 0 && m_of(tau, T / 2) <= n_out;
-      LP4 hw = (LP4)(buf + ln * kHeldRow);
-#pragma unroll
-      for (int k = 0; k < K / 2; ++k) hw[k] = v4f{h[2 * k].x, h[2 * k].y, h[2 * k + 1].x, h[2 * k + 1].y};
-      __builtin_amdgcn_wave_barrier();
-      const LP hr = buf + (ln / K) * kHeldRow + (ln % K);
-      v2f vc[kChunks];
-      constexpr int nw = (kChunks - kLagChunks) / 2;
-      v4f vw[nw];
-      const LP4 hr2 = (LP4)(buf + (ln / 8) * kHeldRow + 2 * (ln % 8));
-#pragma unroll
-      for (int c = 0; c < nw; ++c) vw[c] = hr2[c * (8 * kHeldRow / 2)];
-#pragma unroll
-      for (int c = 2 * nw; c < kChunks; ++c) vc[c] = hr[c * (64 / K) * kHeldRow];
-      if (inside) {
-#pragma unroll
-        for (int c = 0; c < nw; ++c)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vw[c]), orsrc,
-                                                 (uint32_t)(woff(m_of(tau, 128 * c + 2 * ln)) * 8), 0, kStoreAux);
-#pragma unroll
-        for (int c = 2 * nw; c < kChunks - kLagChunks; ++c) st_out(o + woff(m0 + 64 * c), vc[c]);
-      } else {
-#pragma unroll
-        for (int c = 0; c < nw; ++c) {
-          const int m = m_of(tau, 128 * c + 2 * ln);
-          if (m >= 0 && m < n_out) o[woff(m)] = v2f{vw[c].x, vw[c].y};
-          if (m + 1 >= 0 && m + 1 < n_out) o[woff(m + 1)] = v2f{vw[c].z, vw[c].w};
-        }
-#pragma unroll
-        for (int c = 2 * nw; c < kChunks - kLagChunks; ++c)
-          if (m0 + 64 * c >= 0 && m0 + 64 * c < n_out) o[woff(m0 + 64 * c)] = vc[c];
-      }
-#pragma unroll
-      for (int c = kChunks - kLagChunks; c < kChunks; ++c) ((LP)sl->held[c - (kChunks - kLagChunks)])[ln] = vc[c];
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (last) store_held(tau, nullptr);  // the last tile's top state was exact
-    if (s == 0) cnt0 = tau + 1;
-    else if (s == 1) cnt1 = tau + 1;
-    else cnt2 = tau + 1;
-    if (is_last_stage && last) break;
-  }
-}
-
-template <bool MIX, int DT, int FLIP>
-static void xa_fused_launch(const InDesc &in, const XaFuseArgs &a, const float2 *lo, float2 *out,
-                            int frames, const XaTab *tab, hipStream_t st) {
-  hipLaunchKernelGGL((xa_fused_kernel<MIX, DT, FLIP>), dim3((unsigned)((frames + kWaves - 1) / kWaves)),
-                     dim3(64 * kWaves), 0, st, in, a, (const v2f *)lo, (v2f *)out, frames, tab);
-}
-
-static hipError_t xa_fused_dispatch(const InDesc &in, const XaFuseArgs &a, const float2 *lo, bool mix,
-                                    float2 *out, int frames, const XaTab *tab, hipStream_t st) {
-  if (!mix) {
-    if (in.dtype != kInC64 || in.flip) return hipErrorInvalidValue;
-    xa_fused_launch<false, kInC64, 0>(in, a, lo, out, frames, tab, st);
-  } else if (in.dtype == kInC64) {
-    if (in.flip) xa_fused_launch<true, kInC64, 1>(in, a, lo, out, frames, tab, st);
-    else xa_fused_launch<true, kInC64, 0>(in, a, lo, out, frames, tab, st);
-  } else if (in.dtype == kInC32H) {
-    if (in.flip) xa_fused_launch<true, kInC32H, 1>(in, a, lo, out, frames, tab, st);
-    else xa_fused_launch<true, kInC32H, 0>(in, a, lo, out, frames, tab, st);
-  } else if (in.dtype == kInF32R) {
-    if (in.flip) xa_fused_launch<true, kInF32R, 1>(in, a, lo, out, frames, tab, st);
-    else xa_fused_launch<true, kInF32R, 0>(in, a, lo, out, frames, tab, st);
-  } else {
-    if (in.flip) xa_fused_launch<true, kInCU8, 1>(in, a, lo, out, frames, tab, st);
-    else xa_fused_launch<true, kInCU8, 0>(in, a, lo, out, frames, tab, st);
-  }
-  return hipGetLastError();
 }
 
 template <int B, bool MIX, int DT, int FLIP>
@@ -1554,16 +906,6 @@ extern "C" int zfft_debug_xa_stamps(unsigned long long *out) {
 hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix, float2 *out,
                            int frames, const XaTab *tab, hipStream_t st) {
   return xa::xa_dispatch<kXaB>(in, n, lo, mix, out, frames, tab, st);
-}
-
-hipError_t launch_xa_fused(const InDesc &in, int D, const int64_t *n, const float2 *lo, bool mix,
-                           float2 *ring, float2 *out, int frames, const XaTab *tab, hipStream_t st) {
-  if (D < 1 || D > 3) return hipErrorInvalidValue;
-  xa::XaFuseArgs a{};
-  a.D = D;
-  for (int k = 0; k < D; ++k) a.n[k] = (int)n[k];
-  a.ring = (v2f *)ring;
-  return xa::xa_fused_dispatch(in, a, lo, mix, out, frames, tab, st);
 }
 
 }  // namespace zfft

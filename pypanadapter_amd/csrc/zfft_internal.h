@@ -126,11 +126,6 @@ struct XaTab {
 
 hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix,
                            float2 *out, int frames, const XaTab *tab, hipStream_t st);
-// D (1..3) consecutive stages in one launch, n[0..D-1] their input lengths; stage outputs
-// before the last go through per-frame rings: ring holds frames * (D - 1) * kXaRing complex64.
-constexpr int kXaRing = 4096;
-hipError_t launch_xa_fused(const InDesc &in, int D, const int64_t *n, const float2 *lo, bool mix,
-                           float2 *ring, float2 *out, int frames, const XaTab *tab, hipStream_t st);
 
 // "PC" (polyphase cascade) decimator for zoom 8 (pc_kernels.hip, host tables pc_tables.cpp,
 // design model tools/pc_model.py).  The interior of the three zero-phase stages is, exactly,

@@ -397,13 +397,11 @@ struct zfft_plan {
   std::vector<std::string> mark_names;
   std::string names_buf;
   int n_marks = 0;
-  int sched_frames = 0;  // > 0 inside a batched zfft_process: the whole call's frame count
   int path = 0;  // 0 auto, 1 exact blocked pipeline, 2 fused interior + edge windows,
                 // 3 XA tiles (all-pole + FIR + half-rate all-pole), 4 PC (polyphase cascade,
                 // zoom 8)
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
-  DevBuf edge, xk, xa_tab, tws, means, z4, xa_ring, winf;
-  int xa_fuse = 0;  // XA stages per launch (0 auto: kXaFuseAuto)
+  DevBuf edge, xk, xa_tab, tws, means, z4, winf;
   DevBuf pc_tab, pc_edge;  // PC decimator: PcTab; edge maps U0 V0 U1 V1 (floats)
   int pc_lm = -1;          // L mod 8 of the right-edge map in pc_edge (-1: none)
   int pc_R[2] = {}, pc_J[2] = {}, pc_r[2] = {};
@@ -439,13 +437,6 @@ void mark(zfft_plan *p, hipStream_t st, const char *what = "") {
   p->mark_names[p->n_marks] = what;
   (void)hipEventRecord(p->events[p->n_marks++], st);
 }
-
-// Scope of a batched zfft_process call: its batches are scheduled as the whole call.
-struct SchedFrames {
-  zfft_plan *p;
-  SchedFrames(zfft_plan *pl, int frames) : p(pl) { p->sched_frames = frames; }
-  ~SchedFrames() { p->sched_frames = 0; }
-};
 
 // Stage lengths: n_0 = L, n_{k+1} = ceil(n_k / 2)  (decimate(...)[::2]).
 std::vector<int64_t> stage_lengths(int64_t L, int K) {
@@ -625,11 +616,6 @@ int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
 #define ZFFT_WELCH4_CHUNK_MB 0  // chunks of 48/96/192 MB measured 3.1x/1.8x/1.4x slower (cfg5)
 #endif
 constexpr size_t kWelch4ChunkBytes = (size_t)ZFFT_WELCH4_CHUNK_MB << 20;  // 0: one launch set
-constexpr int kXaFuseAuto = 1;   // XA stages per launch by default (measured: DESIGN §3.1)
-#ifndef ZFFT_XA_FUSED_D1
-#define ZFFT_XA_FUSED_D1 0
-#endif
-constexpr bool kXaFusedD1 = ZFFT_XA_FUSED_D1;  // diagnostic build: single stages on the fused kernel
 constexpr int kMaxLoRows = 256;  // LO rows of set_lo_frames (each n_samples x 8 B)
 
 // Edge width (final-stage samples) recomputed exactly, and the exact window length.
@@ -759,34 +745,22 @@ int run_fused(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   return ZFFT_OK;
 }
 
-// XA path: one wave per frame; groups of up to `fuse` consecutive stages per launch (stages
-// inside a group hand over through per-frame rings), group outputs in natural layout.
+// XA path: one wave per frame and stage launch, stage outputs in natural layout (ping /
+// pong).  Two or three stages per launch through per-frame rings measured slower.
 int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t> &n,
            const float2 **out, hipStream_t st) {
-  const int fuse = std::min(p->K, p->xa_fuse > 0 ? p->xa_fuse : kXaFuseAuto);
   hipError_t e = p->ping.ensure((size_t)frames * n[1] * sizeof(float2));
-  if (e == hipSuccess && p->K > fuse) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
-  if (e == hipSuccess && fuse > 1)
-    e = p->xa_ring.ensure((size_t)frames * (fuse - 1) * kXaRing * sizeof(float2));
+  if (e == hipSuccess && p->K > 1) e = p->pong.ensure((size_t)frames * n[2] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   const float2 *cur = nullptr;
-  for (int k = 0, g = 0; k < p->K; ++g) {
-    const int D = std::min(fuse, p->K - k);
-    float2 *dst = (g & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
+  for (int k = 0; k < p->K; ++k) {
+    float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
     const InDesc src = k == 0 ? in : InDesc{cur, n[k], n[k], kInC64, 0};
-    if (D == 1 && !kXaFusedD1) {
-      e = launch_xa_stage(src, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
-                          p->xa_tab.as<XaTab>(), st);
-      if (e != hipSuccess) return hip_fail(e, "xa_stage launch");
-      mark(p, st, k == 0 ? "xa_stage_mix" : "xa_stage");
-    } else {
-      e = launch_xa_fused(src, D, &n[k], p->lo.as<float2>(), k == 0, p->xa_ring.as<float2>(), dst,
-                          frames, p->xa_tab.as<XaTab>(), st);
-      if (e != hipSuccess) return hip_fail(e, "xa_fused launch");
-      mark(p, st, k == 0 ? "xa_fused_mix" : "xa_fused");
-    }
+    e = launch_xa_stage(src, (int)n[k], p->lo.as<float2>(), k == 0, dst, frames,
+                        p->xa_tab.as<XaTab>(), st);
+    if (e != hipSuccess) return hip_fail(e, "xa_stage launch");
+    mark(p, st, k == 0 ? "xa_stage_mix" : "xa_stage");
     cur = dst;
-    k += D;
   }
   *out = cur;
   return ZFFT_OK;
@@ -891,16 +865,17 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  const int sf = std::max(frames, p->sched_frames);
-  if (p->path == 4) {
-    if (!pc_fits(p, L, frames))
-      return fail(ZFFT_EUNSUPPORTED, "PC decimator (path 4) needs zoom 8, frames of >= 16384 "
-                                     "samples and <= 65535 frames per call");
+  if (p->path == 4 && !pc_fits(p, L, frames))
+    return fail(ZFFT_EUNSUPPORTED, "PC decimator (path 4) needs zoom 8, frames of >= 16384 "
+                                   "samples and <= 65535 frames per call");
+  // PC is the fastest schedule wherever it applies, from one frame per call (the
+  // reference's use: 0.083 against 0.37 ms for path 1) to full batches (1024 frames: 1.44
+  // against 2.03 ms for XA) -- tools/sweep_schedule.py, profiles/r04e
+  if (p->path == 4 || (p->path == 0 && pc_fits(p, L, frames)))
     return run_pc(p, in, L, frames, n, out, st);
-  }
-  if (p->path == 3 || (p->path == 0 && auto_xa(sf, L) && xa_fits(p, L)))
+  if (p->path == 3 || (p->path == 0 && auto_xa(frames, L) && xa_fits(p, L)))
     return run_xa(p, in, frames, n, out, st);
-  if (use_fused(p, L, sf)) return run_fused(p, in, L, frames, n, out, st);
+  if (use_fused(p, L, frames)) return run_fused(p, in, L, frames, n, out, st);
   return run_exact(p, in, p->lo.as<float2>(), frames, n, out, st);
 }
 
@@ -1165,7 +1140,7 @@ int zfft_plan_destroy(zfft_plan *p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->in2, &p->yf, &p->ping, &p->pong, &p->rows,
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
-                    &p->tws, &p->means, &p->z4, &p->xa_ring, &p->winf, &p->pc_tab, &p->pc_edge})
+                    &p->tws, &p->means, &p->z4, &p->winf, &p->pc_tab, &p->pc_edge})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->done_ev) (void)hipEventDestroy(p->done_ev);
@@ -1209,13 +1184,6 @@ int zfft_plan_path(zfft_plan *p, int32_t path) {
   if (!p || path < 0 || path > 4)
     return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused), 3 (XA tiles) or 4 (PC)");
   p->path = path;
-  return ZFFT_OK;
-}
-
-int zfft_plan_fuse(zfft_plan *p, int32_t stages) {
-  if (!p || stages < 0 || stages > 3)
-    return fail(ZFFT_EINVAL, "fuse must be 0 (auto) or 1..3 decimation stages per XA launch");
-  p->xa_fuse = stages;
   return ZFFT_OK;
 }
 
@@ -1301,15 +1269,20 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
   // Batches: one for a small call; otherwise >= 2 so that the H2D copy of batch k+1 (copy
   // stream) runs while batch k is computed (plan stream).  From pinned memory both are
   // asynchronous; from pageable memory HIP stages the copy on this thread, which then copies
-  // batch k+1 while the GPU computes batch k.  The decimator schedule of every batch is the
-  // one the whole call would get (SchedFrames), so formats and batchings compare like for
-  // like; batches keep >= kXaMinFrames frames when the call has twice that (fuller waves).
+  // batch k+1 while the GPU computes batch k.  Every batch takes the schedule its own frame
+  // count earns; a call the XA tiles would take keeps them in every batch: its batches hold at
+  // least the XA threshold for this frame length (or the call is one batch), so splitting
+  // never drops a large call onto a schedule that loses at its batch size.
   int B = frames;
   const size_t total = (size_t)frames * frame_bytes;
   if (total >= kPipeMinBytes && frames >= 2) {
     int nb = std::max<int64_t>(2, (int64_t)((total + kPipeBatchBytes - 1) / kPipeBatchBytes));
     B = (frames + nb - 1) / nb;
-    if (frames >= 2 * kXaMinFrames) B = std::max(B, kXaMinFrames);
+    const int need = L <= kXaShortFrame ? kXaMinFramesShort : kXaMinFrames;
+    if (p->path == 0 && p->K > 0 && !pc_fits(p, L, frames) && auto_xa(frames, L) && B < need) {
+      nb = std::max(1, frames / need);
+      B = (frames + nb - 1) / nb;
+    }
   }
   const int nb = (frames + B - 1) / B;
   hipError_t e = p->in.ensure((size_t)B * frame_bytes);
@@ -1322,7 +1295,6 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
   const char *src = (const char *)iq;
   p->n_marks = 0;  // timings cover every batch of this call
   mark(p, p->stream, "start");
-  SchedFrames sched(p, frames);  // each batch gets the schedule of the whole call
   for (int k = 0; k < nb; ++k) {
     const int f0 = k * B, nk = std::min(B, frames - f0), buf = k & 1;
     void *dst = buf ? p->in2.p : p->in.p;

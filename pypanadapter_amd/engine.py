@@ -118,12 +118,9 @@ class ZoomFFT:
         """0 auto, 1 exact reference pass order (blocked; the auto choice for small batches,
         e.g. one frame per call), 2 fused interior + exact edges (blocked; auto from 2^27
         samples per call), 3 XA tiles (all-pole + FIR + half-rate all-pole, one wave per
-        frame; auto for >= 768 frames, or >= 384 frames of <= 2^19 samples)."""
+        frame; auto for >= 768 frames, or >= 384 frames of <= 2^19 samples), 4 PC polyphase
+        cascade (zoom 8, frames >= 16384 samples; the auto choice there at every batch)."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
-
-    def set_fuse(self, stages: int) -> None:
-        """XA decimation stages per launch: 0 auto, 1 one launch per stage, 2-3 fused (rings)."""
-        check(self.lib.zfft_plan_fuse(self._plan, int(stages)), "zfft_plan_fuse")
 
     def set_welch(self, mode: int) -> None:
         """0 auto, 1 one workgroup per frame (n_fft <= 16384), 2 four-step (n_fft >= 4096)."""

@@ -103,6 +103,13 @@ class Waterfall:
     does; the reference then plots that same stamped row, S:2130), writes it as the new
     line, rolls by `scroll` and stamps the tick marks.  `img_array` materialises the
     image in the reference's row order (float64, like the reference's array).
+
+    The device ring holds float32 (half the HBM and PCIe of float64 per line; the GPU
+    rows are float32 anyway).  A float64 row from the reference's own pipeline (its psd is
+    float64, S:2106) is stored as its float32 rounding, so `img_array` equals the
+    reference's image exactly for float32-representable rows and within half a float32 ulp
+    (<= 7.6e-6 dB for |dB| < 256) otherwise; the grid stamps (0) and the -500 fill are exact.
+    Pinned by tests/test_gpu_parity.py::test_waterfall_float64_rows_are_held_as_float32.
     """
 
     def __init__(self, scroll: int = 1, device: int = 0, fs: float = 2.4e6):
@@ -128,6 +135,13 @@ class Waterfall:
     def init_image(self):
         if self._plan is not None:
             self._plan.waterfall_reset(self.scroll)
+
+    def close(self):
+        """Release the device ring (the reference's image is garbage-collected)."""
+        if self._plan is not None:
+            self._plan.close()
+            self._plan = None
+            self.fftwidth = 0
 
     def set_scroll(self, scroll: int):
         """ApplicationDisplay.on_invertscroll_clicked (S:2074-2077): new direction + init."""

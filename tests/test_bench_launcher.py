@@ -25,6 +25,8 @@ def test_gpus_n_spawns_n_ranks(n):
     assert [r["rank"] for r in res["ranks"]] == list(range(n))
     assert [r["local_rank"] for r in res["ranks"]] == list(range(n))
     assert len({r["pid"] for r in res["ranks"]}) == n
+    # each rank's plan on its own GPU: rank r -> cuda:r on one node (no two ranks share a card)
+    assert [r["plan_device"] for r in res["ranks"]] == list(range(n))
 
 
 def test_torchrun_environment_is_honoured():
@@ -43,6 +45,7 @@ def test_torchrun_environment_is_honoured():
     assert len(lines) == 1
     res = json.loads(lines[0])
     assert res["world"] == 2 and sorted(r["local_rank"] for r in res["ranks"]) == [0, 1]
+    assert all(r["plan_device"] == r["local_rank"] for r in res["ranks"])
 
 
 def test_failed_rank_ends_the_others():

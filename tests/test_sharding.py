@@ -69,8 +69,10 @@ def _gpu_worker(rank, world, port, frames, path, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from pypanadapter_amd import ZoomFFT
-    with ZoomFFT(1024, 8, 2.4e6) as plan:  # both ranks on device 0 (the GPU box has one)
+    from pypanadapter_amd import ZoomFFT, device_count
+    dev = rank % device_count()  # rank r on GPU r on a node; both on device 0 on a 1-GPU box
+    with ZoomFFT(1024, 8, 2.4e6, device=dev) as plan:
+        assert plan.device == dev
         plan.set_path(path)
         rows = run_sharded(frames, plan.rows, rank, world, dist=dist)
     if rank == 0:

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Build A/B variants of libzfft.so (kernel build knobs) into pypanadapter_amd/lib/variants/;
-run one with ZFFT_LIB_PATH=<path> python bench.py ...   usage: build_variants.py NAME=D1,D2 ..."""
+run one with ZFFT_LIB_PATH=<path> python bench.py ...   usage: build_variants.py NAME=D1,D2 ...
+Every variant is a diagnostic build (-DZFFT_DIAG: the knobs XA_STAMPS, XA_EXP, PC_KO exist only
+there; the shipped library never has them)."""
 import os
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -12,7 +14,7 @@ from pypanadapter_amd import build  # noqa: E402
 def one(spec):
     name, _, defs = spec.partition("=")
     out = os.path.join(build.LIB_DIR, "variants", f"libzfft_{name}.so")
-    build.build(out=out, defines=tuple(d for d in defs.split(",") if d))
+    build.build(out=out, defines=("ZFFT_DIAG",) + tuple(d for d in defs.split(",") if d))
     return out
 
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-phase cycle shares of the XA stage kernel from a -DXA_STAMPS=1 build
-(tools/build_variants.py stamps=XA_STAMPS=1; run with ZFFT_LIB_PATH=<that lib>).
+(tools/build_variants.py stamps=XA_STAMPS=1 (adds ZFFT_DIAG); run with ZFFT_LIB_PATH=<that lib>).
 Diagnostic only: read the SHARES, not the run time of this build."""
 import ctypes
 import os
