@@ -215,7 +215,9 @@ int zfft_plan_path(zfft_plan *plan, int32_t path);
  * the call's first frame) is mixed with f_lo[(f / frames_per_lo) % n] instead of cfg.f_lo --
  * the reference's mixer (S:2090-2094) with f_demod per IF.  frames_per_lo = 1 interleaves
  * the IFs frame by frame; n = 0 restores cfg.f_lo; n = 1 replaces cfg.f_lo.  The LO table
- * holds n rows of n_samples complex64 (n <= 256).  Waits for the plan's enqueued work. */
+ * holds n rows of n_samples complex64 (n <= 256, at most 4 GiB: ZFFT_ENOMEM beyond).  Zoom 1
+ * never mixes (the reference skips zoomfft at ratio 1, S:2108): n > 1 is ZFFT_EINVAL there.
+ * Waits for the plan's enqueued work. */
 int zfft_plan_set_lo_frames(zfft_plan *plan, const double *f_lo, int32_t n, int32_t frames_per_lo);
 
 /* Welch FFT schedule: 0 = automatic (one workgroup per frame for n_fft <= 16384, four-step

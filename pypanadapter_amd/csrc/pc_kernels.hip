@@ -19,7 +19,7 @@
 
 // Diagnostic builds only (ZFFT_DIAG=1, never set by build.py): PC_KO timing knockouts with
 // wrong results by design -- 1 own-rate sections, 2 FIR gamma, 4 output-rate sections,
-// 8 K1's LO mix (and its table loads).
+// 8 K1's LO mix (and its table loads); KW only: 16 the two input-rate FIRs, 32 the input loads.
 #ifndef ZFFT_DIAG
 #define ZFFT_DIAG 0
 #endif
@@ -64,33 +64,47 @@ constexpr int kYRow = 10;  // y1: rows of 8 padded to 10
 constexpr int kXRows = kPcK1In / 16;
 __device__ __forceinline__ int xidx(int s) { return (s >> 4) * kXRow + (s & 15); }
 
-// x[n], x[n+1] of frame f (both inside the frame), as complex64
+// x[n], x[n+1] of frame f (both inside the frame): the raw load (issued early by KW's
+// prefetch) and its conversion to complex64
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef unsigned char u8x4 __attribute__((ext_vector_type(4)));
+template <int DT> struct RawP;
+template <> struct RawP<kInC64> { typedef v4f T; };
+template <> struct RawP<kInC32H> { typedef h4 T; };
+template <> struct RawP<kInF32R> { typedef float2 T; };
+template <> struct RawP<kInCU8> { typedef u8x4 T; };
 template <int DT, int FLIP>
-__device__ __forceinline__ void load_pair(const InDesc &in, int64_t f, int64_t n, v2f &a, v2f &b) {
+__device__ __forceinline__ typename RawP<DT>::T raw_pair(const InDesc &in, int64_t f, int64_t n) {
+  typedef typename RawP<DT>::T T;
   const int64_t k = f * in.stride + (FLIP ? in.len - 2 - n : n);  // first raw element
+  if constexpr (DT == kInC64) return *(const T *)((const v2f *)in.p + k);
+  else if constexpr (DT == kInC32H) return *(const T *)((const h2 *)in.p + k);
+  else if constexpr (DT == kInF32R) return *(const T *)((const float *)in.p + k);
+  else return *(const T *)((const u8x2 *)in.p + k);
+}
+template <int DT, int FLIP>
+__device__ __forceinline__ void cvt_pair(typename RawP<DT>::T w, v2f &a, v2f &b) {
   v2f p, q;
   if constexpr (DT == kInC64) {
-    const v4f w = *(const v4f *)((const v2f *)in.p + k);
     p = lo2(w);
     q = hi2(w);
   } else if constexpr (DT == kInC32H) {
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    const h4 w = *(const h4 *)((const h2 *)in.p + k);
     p = v2f{(float)w.x, (float)w.y};
     q = v2f{(float)w.z, (float)w.w};
   } else if constexpr (DT == kInF32R) {
-    const float2 w = *(const float2 *)((const float *)in.p + k);
     p = v2f{w.x, 0.f};
     q = v2f{w.y, 0.f};
   } else {
-    typedef unsigned char u8x4 __attribute__((ext_vector_type(4)));
-    const u8x4 w = *(const u8x4 *)((const u8x2 *)in.p + k);
     const float s = 1.f / 127.5f;
     p = v2f{((float)w.x - 127.5f) * s, ((float)w.y - 127.5f) * s};
     q = v2f{((float)w.z - 127.5f) * s, ((float)w.w - 127.5f) * s};
   }
   a = FLIP ? q : p;
   b = FLIP ? p : q;
+}
+template <int DT, int FLIP>
+__device__ __forceinline__ void load_pair(const InDesc &in, int64_t f, int64_t n, v2f &a, v2f &b) {
+  cvt_pair<DT, FLIP>(raw_pair<DT, FLIP>(in, f, n), a, b);
 }
 
 // One tile: y2 for q in [q_s, q_s + 992), q_s = -16 + 992 tile, from the mixed input
@@ -356,10 +370,289 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
     if (m0 + s < n3) ob[m0 + s] = sp[kOutOff + s];
 }
 
+// ---------------------------------------------------------------------------------- KW
+
+// a shift by 16 lanes toward higher (UP) / lower lanes, 0 where there is no source
+template <bool UP>
+__device__ __forceinline__ v2f shift16(v2f v, int lane) {
+  const v2f r = UP ? shup(v, 16) : shdn(v, 16);
+  return (UP ? lane < 16 : lane >= 48) ? splat(0.f) : r;
+}
+
+// sec_block for KW: own-rate section SI (causal: table wf, B = 16; anticausal: wb, B = 20)
+// over the 4 waves' lane blocks, the waves continuing each other; the first wave in time
+// order enters with (c0, c1): the state carried from the previous tile (causal) or 0.
+template <int B, int LEV, bool UP, int SI>
+__device__ __forceinline__ void wsec(v2f (&v)[B], CT tab0, LP scr, int lane, int wave, v2f c0, v2f c1) {
+  const CT tab = fresh(tab0);
+  CS S = UP ? tab->wf[SI] : tab->wb[SI];
+  const v2f na1 = splat(-S.a1), na2 = splat(-S.a2);
+  v2f y1 = splat(0.f), y2 = splat(0.f);
+#pragma unroll
+  for (int c = 0; c < B; ++c) {
+    const int k = UP ? c : B - 1 - c;
+    const v2f y = vfma(na1, y1, vfma(na2, y2, v[k]));
+    y2 = y1;
+    y1 = y;
+    v[k] = y;
+  }
+  v2f e0 = y1, e1 = y2;
+#pragma unroll
+  for (int d = 0; d < LEV; ++d) {
+    v2f p0, p1;
+    if (d == 0) p0 = wshiftn<UP, 1>(e0), p1 = wshiftn<UP, 1>(e1);
+    else if (d == 1) p0 = wshiftn<UP, 2>(e0), p1 = wshiftn<UP, 2>(e1);
+    else if (d == 2) p0 = wshiftn<UP, 4>(e0), p1 = wshiftn<UP, 4>(e1);
+    else if (d == 3) p0 = wshiftn<UP, 8>(e0), p1 = wshiftn<UP, 8>(e1);
+    else p0 = shift16<UP>(e0, lane), p1 = shift16<UP>(e1, lane);
+    const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
+    e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
+    e0 = n0;
+  }
+  if (lane == (UP ? 63 : 0)) {
+    scr[2 * wave] = e0;
+    scr[2 * wave + 1] = e1;
+  }
+  __syncthreads();
+  const int src = UP ? wave - 1 : wave + 1;
+  v2f s0 = c0, s1 = c1;
+  if (src >= 0 && src < 4) {
+    s0 = scr[2 * src];
+    s1 = scr[2 * src + 1];
+  }
+  {
+    const int dist = UP ? lane : 63 - lane;
+    const float __attribute__((address_space(4))) *x = UP ? &tab->wf_x[SI][dist][0] : &tab->wb_x[SI][dist][0];
+    const v2f n0 = vfma(splat(x[0]), s0, vfma(splat(x[1]), s1, e0));
+    e1 = vfma(splat(x[2]), s0, vfma(splat(x[3]), s1, e1));
+    e0 = n0;
+  }
+  v2f i0 = wshift<UP>(e0), i1 = wshift<UP>(e1);
+  if (lane == (UP ? 0 : 63)) {
+    i0 = s0;
+    i1 = s1;
+  }
+#pragma unroll
+  for (int c = 0; c < B; ++c) {
+    const int k = UP ? c : B - 1 - c;
+    v[k] = vfma(splat(S.ct[c][0]), i0, vfma(splat(S.ct[c][1]), i1, v[k]));
+  }
+}
+
+constexpr int kWZ = 256 * kPcWb;  // own-rate samples held: span s in [256, 5376)
+static_assert(kWZ == kPcK2Span - 256 && 256 * kPcWf == 4 * kPcWQ, "KW geometry");
+static_assert(kOutOff + kPcK2M <= kXRows * kXRow, "KW: u3 + outputs fit the input tile's LDS");
+
+// One workgroup per frame, tiles in order.  Tile tau: outputs [m0, m0 + 2048), m0 = -368 +
+// 2048 tau, K2's span origin 2 m0 - 560 (span index s); its FIR part makes y2 for s in
+// [1280, 5376) (= [4096 tau - 16, + 4096)), four sub-tiles of 1024 from 4128 input samples
+// each (the y1 they share carried in LDS); the causal sections run on those 4096 with the
+// state carried from the previous tile; the anticausal ones on s in [256, 5376) from a zero
+// state at the top (s >= 4938 is warm-up only: 0.935^438 < 1e-12), whose lower 1024 are the
+// previous tile's top causal outputs; then K2's FIR gamma and output-rate sections.
+template <int DT, int FLIP>
+__global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, CT tab) {
+  __shared__ v4f xl4[kXRows * kXRow / 2];  // K1 input tile, then y1; then u3 + staged outputs
+  __shared__ v4f z4[kWZ / 2];              // own-rate samples, span s in [256, 5376)
+  __shared__ v4f scr4[16];                 // cross-wave states (4 section calls)
+  __shared__ v4f car4[2];                  // causal sections' carried states
+  __shared__ v4f y1c4[24];                 // the 48 y1 two sub-tiles share
+  const LP xl = (LP)xl4, zl = (LP)z4, scr = (LP)scr4, car = (LP)car4;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t f = blockIdx.x, L = in.len;
+  const v2f *lor = lo_row(lo, in, f);
+  const v4f lane_lo = *(const v4f *)(lor + 2 * t) * (float)M_SQRT1_2;
+  for (int i = t; i < kPcWQ; i += 256) zl[i] = splat(0.f);
+  if (t < 24) y1c4[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (t < 2) car4[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int ntiles = (int)((n3 - kPcWM0 + kPcWM - 1) / kPcWM);
+  // sub-tile g's first input sample; inside the frame ("fast") its pairs are prefetched into
+  // registers one sub-tile ahead (the first of a tile during the previous tile's sections)
+  auto xs_of = [&](int g) { return 4 * (2 * (int64_t)kPcWM0 + 720 + (int64_t)kPcWQ * g) + 32; };
+  auto fast = [&](int64_t xs) { return xs >= 0 && xs + kPcK1In <= L; };
+  typename RawP<DT>::T pf[9];
+  auto prefetch = [&](int g) {
+    const int64_t xs = xs_of(g);
+    if (g < 4 * ntiles && fast(xs) && !(kKo & 32)) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+        if (i < 8 || t < (kPcK1In - 4096) / 2) pf[i] = raw_pair<DT, FLIP>(in, f, xs + 2 * t + 512 * i);
+    }
+  };
+  prefetch(0);
+  for (int tau = 0; tau < ntiles; ++tau) {
+    const int64_t m0 = kPcWM0 + (int64_t)kPcWM * tau;
+    // ---- FIRs: y2 for s in [1280, 5376), four sub-tiles
+    for (int c = 0; c < 4; ++c) {
+      const int64_t xs = xs_of(4 * tau + c);  // first input sample (y2 from 2 m0 + 720 + 1024 c)
+      if (fast(xs)) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+          const int s = 2 * t + 512 * i;
+          if (i == 8 && t >= (kPcK1In - 4096) / 2) break;
+          v2f a, b;
+          cvt_pair<DT, FLIP>(pf[i], a, b);
+          const v2f cc = lor[xs + 512 * i];  // uniform
+          *(LP4)(xl + xidx(s)) = cat(cmul2(a, cmul2(cc, lo2(lane_lo))), cmul2(b, cmul2(cc, hi2(lane_lo))));
+        }
+        prefetch(4 * tau + c + 1);
+      } else {
+        for (int s = t; s < kPcK1In; s += 256) {
+          const int64_t n = xs + s;
+          v2f v = splat(0.f);
+          if (n >= 0 && n < L) v = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
+          xl[xidx(s)] = v;
+        }
+        prefetch(4 * tau + c + 1);
+      }
+      __syncthreads();
+      v2f acc[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] = splat(0.f);
+      {
+        const LP xb = xl + t * kXRow;
+#pragma unroll
+        for (int p = 0; p < ((kKo & 16) ? 1 : 24); ++p) {
+          const int j = 2 * p;
+          const v4f w = *(LP4)(xb + (j >> 4) * kXRow + (j & 15));
+          const v2f x0 = lo2(w), x1 = hi2(w);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int u = j - 2 * r;
+            if (u >= 0 && u < kPcG0) acc[r] = vfma(splat(tab->g0[u]), x0, acc[r]);
+            if (u + 1 >= 0 && u + 1 < kPcG0) acc[r] = vfma(splat(tab->g0[u + 1]), x1, acc[r]);
+          }
+        }
+      }
+      __syncthreads();
+      // y1 local i <-> 2 Q - 24 + i: [0, 48) carried, thread t's 8 at 48 + 8 t (row 6 + t)
+      const LP yl = xl;
+      if (t < 24) *(LP4)(yl + (t >> 2) * kYRow + 2 * (t & 3)) = y1c4[t];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *(LP4)(yl + (6 + t) * kYRow + 2 * q) = cat(acc[2 * q], acc[2 * q + 1]);
+      __syncthreads();
+      {
+        v2f b[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[r] = splat(0.f);
+        const LP yb = yl + t * kYRow;
+#pragma unroll
+        for (int p = 0; p < ((kKo & 16) ? 1 : 28); ++p) {
+          const int j = 2 * p;
+          const v4f w = *(LP4)(yb + (j >> 3) * kYRow + (j & 7));
+          const v2f x0 = lo2(w), x1 = hi2(w);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int u = j - 2 * r;
+            if (u >= 0 && u < kPcG1) b[r] = vfma(splat(tab->g1[u]), x0, b[r]);
+            if (u + 1 >= 0 && u + 1 < kPcG1) b[r] = vfma(splat(tab->g1[u + 1]), x1, b[r]);
+          }
+        }
+        const LP zo = zl + kPcWQ * (1 + c) + 4 * t;
+        *(LP4)zo = cat(b[0], b[1]);
+        *(LP4)(zo + 2) = cat(b[2], b[3]);
+        if (t < 24) y1c4[t] = *(LP4)(yl + (256 + (t >> 2)) * kYRow + 2 * (t & 3));  // i = 2048 + 2 t
+      }
+      __syncthreads();
+    }
+    // ---- own-rate sections, causal, on the new 4096 (carried states)
+    {
+      v2f v[kPcWf];
+      const LP zb = zl + kPcWQ + kPcWf * t;
+#pragma unroll
+      for (int k = 0; k < kPcWf; ++k) v[k] = zb[k];
+      if constexpr (!(kKo & 1)) {
+        const v2f c0 = car[0], c1 = car[1], c2 = car[2], c3 = car[3];
+        wsec<kPcWf, pc_wf_levels(0), true, 0>(v, tab, scr, lane, wave, c0, c1);
+        if (t == 255) {
+          car[0] = v[kPcWf - 1];
+          car[1] = v[kPcWf - 2];
+        }
+        wsec<kPcWf, pc_wf_levels(1), true, 1>(v, tab, scr + 8, lane, wave, c2, c3);
+        if (t == 255) {
+          car[2] = v[kPcWf - 1];
+          car[3] = v[kPcWf - 2];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kPcWf; ++k) zb[k] = v[k];
+    }
+    __syncthreads();
+    // the next tile's lower 1024 causal outputs (s in [4352, 5376) -> [256, 1280))
+    v2f cz[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cz[r] = zl[4 * kPcWQ + 4 * t + r];
+    // ---- own-rate sections, anticausal, on s in [256, 5376)
+    {
+      v2f v[kPcWb];
+      const LP zb = zl + kPcWb * t;
+#pragma unroll
+      for (int k = 0; k < kPcWb; ++k) v[k] = zb[k];
+      __syncthreads();  // cz read before anything is written back
+      if constexpr (!(kKo & 1)) {
+        wsec<kPcWb, pc_wb_levels(0), false, 0>(v, tab, scr + 16, lane, wave, splat(0.f), splat(0.f));
+        wsec<kPcWb, pc_wb_levels(1), false, 1>(v, tab, scr + 24, lane, wave, splat(0.f), splat(0.f));
+      }
+#pragma unroll
+      for (int k = 0; k < kPcWb; ++k) zb[k] = v[k];
+    }
+    __syncthreads();
+    // ---- FIR gamma (K2's): u3 index k = 9 t + r (output m0 - 128 + k) from z s in [2k + 276, + 56]
+    {
+      v2f u[9];
+#pragma unroll
+      for (int r = 0; r < 9; ++r) u[r] = splat(0.f);
+      const LP zb = zl + 18 * t + (kPcK2Left - 2 * kU3Base) - (kPcG2 - 1) / 2 - 256;
+#pragma unroll
+      for (int p = 0; p < ((kKo & 2) ? 1 : 37); ++p) {
+        const int j = 2 * p;
+        const v4f w = *(LP4)(zb + j);
+        const v2f x0 = lo2(w), x1 = hi2(w);
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+          const int q = j - 2 * r;
+          if (q >= 0 && q < kPcG2) u[r] = vfma(splat(tab->g2[q]), x0, u[r]);
+          if (q + 1 >= 0 && q + 1 < kPcG2) u[r] = vfma(splat(tab->g2[q + 1]), x1, u[r]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 9; ++r) xl[9 * t + r] = u[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) zl[4 * t + r] = cz[r];
+    // ---- output-rate sections (K2's: wave q takes outputs [512 q, + 512) with halos)
+    {
+      v2f a[kPcApBlk];
+      const int k0 = kU3Base - kPcApHalo + (kPcK2M / 4) * wave + kPcApBlk * lane;
+#pragma unroll
+      for (int i = 0; i < kPcApBlk; ++i) a[i] = xl[k0 + i];
+      if constexpr (!(kKo & 4)) {
+        ap_cascade<0, true>(a, tab, lane);
+        ap_cascade<0, false>(a, tab, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < kPcApBlk; ++i) {
+        const int k = k0 + i - kU3Base;
+        const int q = k - (kPcK2M / 4) * wave;
+        if (q >= 0 && q < kPcK2M / 4) xl[kOutOff + k] = a[i];
+      }
+    }
+    __syncthreads();
+    v2f *ob = out + f * n3;
+    for (int s = t; s < kPcK2M; s += 256) {
+      const int64_t m = m0 + s;
+      if (m >= 0 && m < n3) ob[m] = xl[kOutOff + s];
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------------- K3
 
 // out[m] += sum_k U[m][k] (sum_j V[j][k] x[j]): side 0 from the frame start, side 1 from
-// its end (x[j] = mixed input L-1-j, out index n3-1-m).  One block per frame and side.
+// its end (x[j] = mixed input L-1-j, out index n3-1-m).  One block per frame and side; V is
+// uploaded transposed (r x J) so a wave's V loads are coalesced.
 template <int DT, int FLIP>
 __global__ void __launch_bounds__(256) pc_edge_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3,
                                                       const float *U0, const float *V0, int R0, int J0,
@@ -380,7 +673,7 @@ __global__ void __launch_bounds__(256) pc_edge_kernel(InDesc in, const v2f *lo, 
     const v2f x = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
 #pragma unroll
     for (int k = 0; k < kPcEdgeRank; ++k)
-      if (k < r) acc[k] = vfma(splat(V[(int64_t)j * r + k]), x, acc[k]);
+      if (k < r) acc[k] = vfma(splat(V[(int64_t)k * J + j]), x, acc[k]);  // V stored r x J
   }
 #pragma unroll
   for (int k = 0; k < kPcEdgeRank; ++k) {
@@ -432,6 +725,13 @@ hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int6
   const dim3 grid((unsigned)((n3 + kPcK2M - 1) / kPcK2M), frames);
   hipLaunchKernelGGL(pc::pc_tail_kernel, grid, dim3(256), 0, st, (const v2f *)y2, y2_stride,
                      y2_stride, (v2f *)out, n3, (pc::CT)tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_pc_walk(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
+                          const PcTab *tab, hipStream_t st) {
+  PC_DISPATCH(pc::pc_walk_kernel, in, dim3((unsigned)frames), dim3(256), 0, st, in, (const v2f *)lo,
+              (v2f *)out, n3, (pc::CT)tab);
   return hipGetLastError();
 }
 

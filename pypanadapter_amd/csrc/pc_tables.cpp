@@ -111,7 +111,7 @@ bool sec_tables(double a1, double a2, int B, int levels, int dcut, PcSec &s) {
   s.a2 = (float)a2;
   s.pad_[0] = s.pad_[1] = 0.f;
   const M2 A = {{-a1, -a2}, {1.0, 0.0}};
-  for (int d = 0; d < 4; ++d) {
+  for (int d = 0; d < 5; ++d) {
     M2 P;
     pow2(A, B << d, P);
     for (int i = 0; i < 4; ++i) s.pw[d][i] = (float)P[i / 2][i % 2];
@@ -283,13 +283,21 @@ bool pc_build_tables(PcTab &tab) {
   const int own_idx[kPcOwn] = {2, 3};
   for (int s = 0; s < kPcOwn; ++s) {
     const double a1 = l.d[0].a1[own_idx[s]], a2 = l.d[0].a2[own_idx[s]];
-    if (!sec_tables(a1, a2, kPcOwnBlk, pc_own_levels(s), kPcOwnBlk, tab.own[s])) return false;
+    if (!sec_tables(a1, a2, kPcOwnBlk, pc_own_levels(s), kPcOwnBlk, tab.own[s]) ||
+        !sec_tables(a1, a2, kPcWf, pc_wf_levels(s), kPcWf, tab.wf[s]) ||
+        !sec_tables(a1, a2, kPcWb, pc_wb_levels(s), kPcWb, tab.wb[s]))
+      return false;
     const M2 A = {{-a1, -a2}, {1.0, 0.0}};
-    for (int i = 0; i < 64; ++i) {
-      M2 P;
-      pow2(A, kPcOwnBlk * (i + 1), P);
-      for (int q = 0; q < 4; ++q) tab.own_x[s][i][q] = (float)P[q / 2][q % 2];
-    }
+    auto cross = [&](int B, float (*x)[4]) {
+      for (int i = 0; i < 64; ++i) {
+        M2 P;
+        pow2(A, B * (i + 1), P);
+        for (int q = 0; q < 4; ++q) x[i][q] = (float)P[q / 2][q % 2];
+      }
+    };
+    cross(kPcOwnBlk, tab.own_x[s]);
+    cross(kPcWf, tab.wf_x[s]);
+    cross(kPcWb, tab.wb_x[s]);
   }
   // output-rate sections: D8 (stage 0), D4 (stage 1), D2 sections 0, 1 (stage 2), slowest
   // first

@@ -138,7 +138,10 @@ hipError_t launch_xa_stage(const InDesc &in, int n, const float2 *lo, bool mix,
 // on the zero-extended frame; the frame ends (odd extension, sosfilt_zi states) add a
 // low-rank linear map of the first / last input samples onto the first / last outputs.
 // K1 = the two FIRs (independent tiles) -> y2 in device memory; K2 = the rest (independent
-// tiles with warm-up halos); K3 = the edge maps.
+// tiles with warm-up halos); K3 = the edge maps.  KW ("walk") = K1 + K2 in one launch, one
+// workgroup per frame walking its tiles in order: y2 stays in LDS, the causal own-rate
+// sections carry their state from tile to tile (no warm-up halo), the anticausal ones warm
+// up over the next tile's first 1024 own-rate samples (the output tile lags the FIR tile).
 constexpr int kPcStages = 3;              // zoom 8 only
 constexpr int kPcQ0 = -16;                // first y2 index of the model's support
 constexpr int kPcK1Q = 992;               // y2 outputs per K1 tile
@@ -158,7 +161,7 @@ constexpr int kPcEdgeR = 192, kPcEdgeJ = 1536, kPcEdgeRank = 16;  // edge map ca
 constexpr int kPcCt = 24;                 // zero-input response rows (>= both block lengths)
 struct PcSec {
   float a1, a2, pad_[2];
-  float pw[4][4];
+  float pw[5][4];
   float ct[kPcCt][2];
 };
 struct PcTab {
@@ -166,7 +169,15 @@ struct PcTab {
   PcSec own[kPcOwn];                // B = 21 (stage 2's sections 2, 3)
   float own_x[kPcOwn][64][4];       // A^(21 (i + 1)) for lane i (cross-wave scan step)
   PcSec ap[kPcAp];                  // B = 11, slowest first
+  PcSec wf[kPcOwn], wb[kPcOwn];     // KW own-rate sections: causal B = 16, anticausal B = 20
+  float wf_x[kPcOwn][64][4], wb_x[kPcOwn][64][4];  // A^(B (i + 1)) for those
 };
+constexpr int kPcWf = 16, kPcWb = 20;    // KW own-rate block lengths (4096 / 5120 samples)
+constexpr int kPcWM = 2048;              // KW outputs per tile (= kPcK2M: K2's geometry)
+constexpr int kPcWQ = 1024;              // KW y2 per FIR sub-tile (4 per tile)
+constexpr int kPcWM0 = -368;             // KW first tile's m0: its FIR tile starts at kPcQ0
+__host__ __device__ constexpr int pc_wf_levels(int s) { return s == 0 ? 3 : 5; }
+__host__ __device__ constexpr int pc_wb_levels(int s) { return s == 0 ? 3 : 4; }
 // Scan levels and correction lengths the kernels are compiled for (checked by the builder).
 __host__ __device__ constexpr int pc_own_levels(int s) { return s == 0 ? 3 : 4; }
 __host__ __device__ constexpr int pc_ap_levels(int s) {
@@ -187,6 +198,8 @@ hipError_t launch_pc_fir(const InDesc &in, const float2 *lo, float2 *y2, int64_t
                          int frames, const PcTab *tab, hipStream_t st);
 hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int64_t n3,
                           int frames, const PcTab *tab, hipStream_t st);
+hipError_t launch_pc_walk(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
+                          const PcTab *tab, hipStream_t st);
 // both frame ends in one launch: [0] = start, [1] = end
 hipError_t launch_pc_edge(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
                           const float *const U[2], const float *const V[2], const int R[2],

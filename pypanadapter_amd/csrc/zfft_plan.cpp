@@ -12,6 +12,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -470,6 +471,7 @@ constexpr int kWelchOneWgMax = ZFFT_WELCH_ONEWG_MAX;  // auto Welch: one workgro
 
 // LO table: one row of lo_len entries per LO frequency (the plan's f_lo, or the
 // zfft_plan_set_lo_frames list), rows lo_len apart.
+constexpr size_t kMaxLoBytes = (size_t)4 << 30;  // the LO table, all rows
 int ensure_lo(zfft_plan *p, int64_t L) {
   if (p->lo_len >= L) return ZFFT_OK;
   int rc = quiesce(p);
@@ -477,7 +479,14 @@ int ensure_lo(zfft_plan *p, int64_t L) {
   // the XA kernels read lo[lane] for every lane; rows 64-entry aligned
   const int64_t cap = (std::max<int64_t>(L, 64) + 63) & ~(int64_t)63;
   const std::vector<double> freqs = p->lo_freqs.empty() ? std::vector<double>{p->cfg.f_lo} : p->lo_freqs;
-  std::vector<float2> h(cap * freqs.size());
+  if ((double)cap * (double)freqs.size() * sizeof(float2) > (double)kMaxLoBytes)
+    return fail(ZFFT_ENOMEM, "LO table (set_lo_frames rows x frame length x 8 B) over 4 GiB");
+  std::vector<float2> h;
+  try {
+    h.resize(cap * freqs.size());
+  } catch (const std::bad_alloc &) {
+    return fail(ZFFT_ENOMEM, "LO table host staging allocation failed");
+  }
   const double sq2 = std::sqrt(2.0);
   for (size_t k = 0; k < freqs.size(); ++k) {
     const double r = freqs[k] / p->cfg.fs;
@@ -769,6 +778,12 @@ int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t
 // PC decimator (pc_kernels.hip): zoom 8, frames long enough that the two frame ends'
 // maps do not meet (kPcMinL), grid y = frames.
 constexpr int64_t kPcMinL = 16384;
+// KW (one workgroup per frame) from this many frames per call; below, K1 + K2's tiles.
+// tools/sweep_schedule.py (profiles/r04l/sweep_schedule.json, KW / tiles time per call,
+// 299,008-sample frames): 64 frames 3.37, 512 1.03, 1024 1.04, 2048 1.02, 4096 0.987
+// (2^20-sample frames 2048: 1.02): one workgroup per frame needs >= 8 rounds of the chip's
+// 512 resident workgroups to fill it; KW also keeps y2 (2 B per input sample) off HBM.
+constexpr int kPcWalkMinFrames = 4096;
 bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == kPcStages && L >= kPcMinL && frames <= 65535;
 }
@@ -817,8 +832,10 @@ int ensure_pc(zfft_plan *p, int64_t L) {
     p->pc_r[s] = es[s]->r;
     p->pc_off[2 * s] = h.size();
     h.insert(h.end(), es[s]->U.begin(), es[s]->U.end());
-    p->pc_off[2 * s + 1] = h.size();
-    h.insert(h.end(), es[s]->V.begin(), es[s]->V.end());
+    p->pc_off[2 * s + 1] = h.size();  // V transposed to r x J: lanes j read consecutive floats
+    const int J = es[s]->J, r = es[s]->r;
+    for (int k = 0; k < r; ++k)
+      for (int j = 0; j < J; ++j) h.push_back(es[s]->V[(size_t)j * r + k]);
   }
   hipError_t e = p->pc_edge.ensure(h.size() * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(p->pc_edge.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice);
@@ -830,21 +847,30 @@ int ensure_pc(zfft_plan *p, int64_t L) {
 // PC path: K1 (FIRs) -> y2 (ping) -> K2 (own-rate sections, FIR, output-rate sections) ->
 // out (pong) -> K3 (frame-end maps, in place).
 int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vector<int64_t> &n,
-           const float2 **out, hipStream_t st) {
+           bool walk, const float2 **out, hipStream_t st) {
   int rc = ensure_pc(p, L);
   if (rc) return rc;
   const int64_t n3 = n[p->K];
-  const int64_t y2s = (pc_y2_len(L) + kPcK1Q - 1) / kPcK1Q * kPcK1Q;
-  hipError_t e = p->ping.ensure((size_t)frames * y2s * sizeof(float2));
-  if (e == hipSuccess) e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
-  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   const PcTab *tab = p->pc_tab.as<PcTab>();
-  e = launch_pc_fir(in, p->lo.as<float2>(), p->ping.as<float2>(), y2s, frames, tab, st);
-  if (e != hipSuccess) return hip_fail(e, "pc_fir launch");
-  mark(p, st, "pc_fir");
-  e = launch_pc_tail(p->ping.as<float2>(), y2s, p->pong.as<float2>(), n3, frames, tab, st);
-  if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
-  mark(p, st, "pc_tail");
+  hipError_t e;
+  if (walk) {  // one launch, y2 in LDS
+    e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+    e = launch_pc_walk(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, tab, st);
+    if (e != hipSuccess) return hip_fail(e, "pc_walk launch");
+    mark(p, st, "pc_walk");
+  } else {
+    const int64_t y2s = (pc_y2_len(L) + kPcK1Q - 1) / kPcK1Q * kPcK1Q;
+    e = p->ping.ensure((size_t)frames * y2s * sizeof(float2));
+    if (e == hipSuccess) e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+    e = launch_pc_fir(in, p->lo.as<float2>(), p->ping.as<float2>(), y2s, frames, tab, st);
+    if (e != hipSuccess) return hip_fail(e, "pc_fir launch");
+    mark(p, st, "pc_fir");
+    e = launch_pc_tail(p->ping.as<float2>(), y2s, p->pong.as<float2>(), n3, frames, tab, st);
+    if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
+    mark(p, st, "pc_tail");
+  }
   const float *eb = p->pc_edge.as<float>();
   const float *const U[2] = {eb + p->pc_off[0], eb + p->pc_off[2]};
   const float *const V[2] = {eb + p->pc_off[1], eb + p->pc_off[3]};
@@ -865,14 +891,15 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  if (p->path == 4 && !pc_fits(p, L, frames))
-    return fail(ZFFT_EUNSUPPORTED, "PC decimator (path 4) needs zoom 8, frames of >= 16384 "
+  if ((p->path == 4 || p->path == 5) && !pc_fits(p, L, frames))
+    return fail(ZFFT_EUNSUPPORTED, "PC decimator (paths 4, 5) needs zoom 8, frames of >= 16384 "
                                    "samples and <= 65535 frames per call");
   // PC is the fastest schedule wherever it applies, from one frame per call (the
   // reference's use: 0.083 against 0.37 ms for path 1) to full batches (1024 frames: 1.44
-  // against 2.03 ms for XA) -- tools/sweep_schedule.py, profiles/r04e
-  if (p->path == 4 || (p->path == 0 && pc_fits(p, L, frames)))
-    return run_pc(p, in, L, frames, n, out, st);
+  // against 2.03 ms for XA) -- tools/sweep_schedule.py, profiles/r04l
+  if (p->path == 4 || p->path == 5 || (p->path == 0 && pc_fits(p, L, frames)))
+    return run_pc(p, in, L, frames, n, p->path == 5 || (p->path == 0 && frames >= kPcWalkMinFrames),
+                  out, st);
   if (p->path == 3 || (p->path == 0 && auto_xa(frames, L) && xa_fits(p, L)))
     return run_xa(p, in, frames, n, out, st);
   if (use_fused(p, L, frames)) return run_fused(p, in, L, frames, n, out, st);
@@ -1181,8 +1208,9 @@ int zfft_plan_timing(zfft_plan *p, int32_t enable) {
 }
 
 int zfft_plan_path(zfft_plan *p, int32_t path) {
-  if (!p || path < 0 || path > 4)
-    return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused), 3 (XA tiles) or 4 (PC)");
+  if (!p || path < 0 || path > 5)
+    return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused), 3 (XA tiles), 4 (PC "
+                             "tiles) or 5 (PC walk)");
   p->path = path;
   return ZFFT_OK;
 }
@@ -1192,6 +1220,8 @@ int zfft_plan_set_lo_frames(zfft_plan *p, const double *f_lo, int32_t n, int32_t
   if (rc) return rc;
   if (n < 0 || n > kMaxLoRows || (n > 0 && (!f_lo || frames_per_lo < 1)))
     return fail(ZFFT_EINVAL, "set_lo_frames: 0 <= n <= 256 frequencies, frames_per_lo >= 1");
+  if (n > 1 && p->K == 0)  // rows never mix at zoom 1: the reference skips zoomfft (S:2108)
+    return fail(ZFFT_EINVAL, "set_lo_frames: several LO rows need zoom > 1 (zoom 1 does not mix)");
   for (int i = 0; i < n; ++i)
     if (!std::isfinite(f_lo[i])) return fail(ZFFT_EINVAL, "set_lo_frames: f_lo must be finite");
   rc = quiesce(p);  // the old table may still be read by enqueued work

@@ -129,7 +129,8 @@ class ZoomFFT:
     def set_lo_frames(self, f_lo, frames_per_lo: int = 1) -> None:
         """Batched multi-IF (config 4): frame f of each call is mixed with
         f_lo[(f // frames_per_lo) % len(f_lo)] (the reference's f_demod per IF, S:2090);
-        an empty list restores the plan's f_lo."""
+        an empty list restores the plan's f_lo.  Zoom 1 never mixes (S:2108): several
+        rows raise ValueError there."""
         arr = np.ascontiguousarray(f_lo, dtype=np.float64).ravel()
         check(self.lib.zfft_plan_set_lo_frames(self._plan, arr.ctypes.data_as(ctypes.c_void_p) if arr.size else None,
                                                int(arr.size), int(frames_per_lo)), "zfft_plan_set_lo_frames")

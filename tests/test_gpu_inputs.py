@@ -109,7 +109,7 @@ def _audio(L, fs, seed):
 
 REAL_CASES = [(1024, 1, 1024, 12 * 1024), (1024, 1, 512, 12 * 1024), (2048, 1, 256, 9000),
               (4096, 1, 4096, 40000), (256, 1, 256, 300), (1024, 4, 256, 64 * 1024),
-              (2048, 2, 1024, 30000)]
+              (2048, 2, 1024, 30000), (16384, 1, 16384, 70000)]
 
 
 @pytest.mark.parametrize("N,z,W,L", REAL_CASES, ids=[f"N{c[0]}_z{c[1]}_W{c[2]}_L{c[3]}" for c in REAL_CASES])

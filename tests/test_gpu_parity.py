@@ -227,6 +227,23 @@ def test_welch_one_workgroup_forms_vs_oracle(oracle_lib, N, z, W, F):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, z, W), f"N={N} W={W} frame {f}")
 
 
+@pytest.mark.parametrize("welch", [0, 1, 2])
+@pytest.mark.parametrize("N,z,W", [(16384, 1, 16384), (16384, 2, 8192), (16384, 1, 12000)])
+def test_welch_16384_unpruned_vs_oracle(oracle_lib, welch, N, z, W):
+    """N = 16384 where the crop keeps more than the last stage's outputs 0 and RL-1 (zoom 1
+    with the full row, zoom 2, a ragged W): the full DIF<16384> form (one 1024-thread frame,
+    139 KB of LDS) that the automatic choice (welch 0) takes, the one-workgroup mode and
+    the four-step form, all against the float64 oracle."""
+    from pypanadapter_amd import ZoomFFT
+    L = N * z * 4 + 123
+    x = _frames(2, L, N, z, W, seed0=9900 + z + W // 1000)
+    with ZoomFFT(N, z, 2.4e6, n_win=W) as plan:
+        plan.set_welch(welch)
+        rows = plan.rows(x)
+    for f in range(2):
+        assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, z, W), f"welch={welch} W={W} frame {f}")
+
+
 @pytest.mark.parametrize("N,z,W", [(32768, 8, 4096), (32768, 8, 4100), (65536, 16, 4096),
                                    (65536, 8, 8200), (16384, 8, 2048), (8192, 8, 1024),
                                    (4096, 8, 512), (16384, 4, 4096)])
@@ -521,6 +538,17 @@ def test_lo_per_frame_every_schedule(oracle_lib, path, per):
     ref = oracle_lib.zoomfft(x[5], 8, 2.4e6, f_lo=IF_LOS[0])
     assert np.abs(d - ref).max() / np.abs(ref).max() < 3e-5
     assert_row_close(row0, oracle_lib.psd_row(x[7], 2.4e6, 1024, 8, 128), "restored f_lo")
+
+
+def test_lo_rows_refused_at_zoom_1():
+    """Zoom 1 never mixes (the reference skips zoomfft at ratio 1, S:2108): several LO rows
+    would be ignored by the rows, so the plan refuses them; one row (a new f_lo) is kept."""
+    from pypanadapter_amd import ZoomFFT
+    with ZoomFFT(1024, 1, 2.4e6) as plan:
+        with pytest.raises(ValueError):
+            plan.set_lo_frames([1.0, 2.0], 1)
+        plan.set_lo_frames([5.0], 1)
+        plan.set_lo_frames([], 1)
 
 
 @pytest.mark.parametrize("path,first", [(0, "pc_fir"), (3, "xa_stage_mix")])

@@ -12,6 +12,8 @@ from conftest import assert_row_close, case_input, golden_cases, golden_rows
 
 pytestmark = pytest.mark.gpu
 PC_TOL = 1e-5
+# 4: K1 + K2 tiles (y2 through device memory), 5: KW (one workgroup walks each frame)
+PC_PATHS = pytest.mark.parametrize("path", [4, 5], ids=["tiles", "walk"])
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -33,14 +35,15 @@ PC_LENGTHS = [16384, 16385, 16386, 16387, 16388, 16389, 16390, 16391, 3968 * 5 +
 
 
 @pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
-def test_pc_decimate_vs_oracle(oracle_lib, flip):
+@PC_PATHS
+def test_pc_decimate_vs_oracle(oracle_lib, flip, path):
     from pypanadapter_amd import ZoomFFT
     rng = np.random.default_rng(4400 + flip)
     for L in PC_LENGTHS:
         x = (rng.standard_normal(L) + 1j * rng.standard_normal(L)).astype(np.complex64)
         x += np.exp(2j * np.pi * 0.0071 * np.arange(L)).astype(np.complex64)
         with ZoomFFT(4096, 8, 2.4e6, flip=flip) as plan:
-            plan.set_path(4)
+            plan.set_path(path)
             d = plan.decimate(x)
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 8, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
@@ -50,18 +53,20 @@ def test_pc_decimate_vs_oracle(oracle_lib, flip):
 
 @pytest.mark.parametrize("N,L,F", [(4096, 299008, 6), (16384, 294912, 3), (65536, 1048576, 2),
                                     (1024, 65536, 4), (32768, 524288 + 3, 2)])
-def test_pc_rows_vs_oracle(oracle_lib, N, L, F):
+@PC_PATHS
+def test_pc_rows_vs_oracle(oracle_lib, N, L, F, path):
     from pypanadapter_amd import ZoomFFT
     W = N // 8
     x = _frames(F, L, N, 8, W, seed0=5100 + N // 1024)
     with ZoomFFT(N, 8, 2.4e6, n_win=W) as plan:
-        plan.set_path(4)
+        plan.set_path(path)
         rows = plan.rows(x)
     for f in range(F):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, 8, W), f"N={N} L={L} frame {f}")
 
 
-def test_pc_golden_rows():
+@PC_PATHS
+def test_pc_golden_rows(path):
     """Every zoom-8 golden row the reference recorded whose frame PC takes (>= 16384)."""
     from pypanadapter_amd import ZoomFFT
     from conftest import window_of
@@ -72,7 +77,7 @@ def test_pc_golden_rows():
         x = case_input(c)
         with ZoomFFT(c["n_fft"], 8, c["fs"], n_win=c["n_win"], window=window_of(c["window"]),
                      f_lo=c["f_lo"]) as plan:
-            plan.set_path(4)
+            plan.set_path(path)
             row = plan.rows(x)
         assert_row_close(row, golden_rows()[c["name"]], c["name"])
         n += 1
@@ -95,7 +100,8 @@ def _encode(x, fmt):
 
 @pytest.mark.parametrize("fmt", ["complex32", "cu8", "f32"])
 @pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
-def test_pc_input_formats(oracle_lib, fmt, flip):
+@PC_PATHS
+def test_pc_input_formats(oracle_lib, fmt, flip, path):
     """The raw-source formats (complex32 / RTL-SDR u8 / AudioPan real f32) and np.flip fused
     into the K1 loads and the frame-end maps' loads."""
     from pypanadapter_amd import ZoomFFT
@@ -104,21 +110,22 @@ def test_pc_input_formats(oracle_lib, fmt, flip):
     arr, vals = _encode(x, fmt)
     ref_in = vals[:, ::-1] if flip else vals
     with ZoomFFT(N, 8, 2.4e6, n_win=512, in_dtype=fmt, flip=flip) as plan:
-        plan.set_path(4)
+        plan.set_path(path)
         rows = plan.rows(arr)
     for f in range(F):
         assert_row_close(rows[f], oracle_lib.psd_row(ref_in[f], 2.4e6, N, 8, 512),
                          f"{fmt} flip={flip} frame {f}")
 
 
-def test_pc_lo_per_frame(oracle_lib):
+@PC_PATHS
+def test_pc_lo_per_frame(oracle_lib, path):
     """Config 4 on one plan: frame f mixed with f_lo[f % 3] in K1 and the edge maps."""
     from pypanadapter_amd import ZoomFFT
     f_lo = [1.0, 150e3 + 1.0, -300e3 + 1.0]
     L, F = 299008, 6
     x = np.stack([_frames(1, L, 4096, 8, 512, seed0=6500 + f, f_lo=f_lo[f % 3])[0] for f in range(F)])
     with ZoomFFT(4096, 8, 2.4e6, n_win=512) as plan:
-        plan.set_path(4)
+        plan.set_path(path)
         plan.set_lo_frames(f_lo, 1)
         rows = plan.rows(x)
     for f in range(F):
@@ -132,37 +139,40 @@ def test_pc_matches_xa_and_exact_rows(oracle_lib):
     from pypanadapter_amd import ZoomFFT
     x = _frames(4, 299008, 4096, 8, 512, seed0=6900)
     out = {}
-    for path in (1, 3, 4):
+    for path in (1, 3, 4, 5):
         with ZoomFFT(4096, 8, 2.4e6) as plan:
             plan.set_path(path)
             out[path] = (plan.rows(x), plan.decimate(x[1]))
-    a, b = out[4][1], out[1][1]
-    assert np.abs(a - b).max() / np.abs(b).max() < PC_TOL
+    for p in (4, 5):
+        a, b = out[p][1], out[1][1]
+        assert np.abs(a - b).max() / np.abs(b).max() < PC_TOL
     for f in range(4):
         ref = oracle_lib.psd_row(x[f], 2.4e6, 4096, 8, 512)
-        for path in (1, 3, 4):
+        for path in (1, 3, 4, 5):
             assert_row_close(out[path][0][f], ref, f"path {path} frame {f}")
 
 
-def test_pc_refuses_outside_its_domain():
+@PC_PATHS
+def test_pc_refuses_outside_its_domain(path):
     from pypanadapter_amd import ZoomFFT
     x = np.zeros(299008, np.complex64)
     with ZoomFFT(4096, 4, 2.4e6) as plan:
-        plan.set_path(4)
+        plan.set_path(path)
         with pytest.raises(NotImplementedError):
             plan.rows(x)
     with ZoomFFT(1024, 8, 2.4e6) as plan:
-        plan.set_path(4)
+        plan.set_path(path)
         with pytest.raises(NotImplementedError):
             plan.rows(np.zeros(16383, np.complex64))
 
 
-def test_pc_size_independent_properties():
+@PC_PATHS
+def test_pc_size_independent_properties(path):
     """Determinism, frame-order equivariance and exact x2 scaling (+12.04 dB) at a batch."""
     from pypanadapter_amd import ZoomFFT
     x = _frames(12, 299008, 4096, 8, 512, seed0=7300)
     with ZoomFFT(4096, 8, 2.4e6) as plan:
-        plan.set_path(4)
+        plan.set_path(path)
         a = plan.rows(x)
         b = plan.rows(x)
         perm = np.random.default_rng(1).permutation(12)

@@ -18,9 +18,12 @@ last stage stays at its own rate; moving it to the output rate amplified fp32 ro
 
 Kernel structure modelled here:
   K1 tiles: 992 y2 outputs per tile from 4128 input samples (FIR alpha then beta).
-  K2 tiles: 2048 outputs per tile from a 5376-sample y2 span (own-rate section over
-        256 thread blocks of 21 with a block scan; FIR gamma; the 11-section cascade over
-        64 lane blocks of 36 with block scans), edges by the matrices.
+  K2 tiles: 2048 outputs per tile from a 5376-sample y2 span (own-rate sections over
+        256 thread blocks of 21 with block scans and cross-wave steps; FIR gamma; the
+        10-section cascade on 4 waves, each a quarter of the tile with 96-sample halos
+        over 64 lane blocks of 11), edges by the matrices.
+  (KW, the walk kernel, runs the same arithmetic with tiles in frame order: the causal
+  own-rate sections carry state instead of the left halo -- same values to fp32 rounding.)
 """
 import numpy as np
 import scipy.signal as ss
@@ -129,9 +132,10 @@ Q0 = -16           # first y2 index (support of the model)
 K1_Q = 992         # y2 outputs per K1 tile
 K2_M = 2048        # outputs per K2 tile
 K2_SPAN = 5376     # y2 samples per K2 tile (256 x 21)
-K2_LEFT = 520      # span starts at 2 m0 - K2_LEFT
-AP_HALO = 80
-AP_BLK = 36
+K2_LEFT = 560      # span starts at 2 m0 - K2_LEFT
+AP_HALO = 96
+AP_BLK = 11
+U3_BASE = 128      # u3 index k <-> output m0 - 128 + k
 
 
 def stage_len(L, k=K):
@@ -198,18 +202,23 @@ def k2(y2, n3, dt=complex):
         for tab in OWN_TABS:                                       # anticausal
             X = block_section(X, tab, dt=dt)
         z2 = X[::-1, ::-1].reshape(-1)
-        # u3[m0 - 80 + k], k in [0, 2304): z2 local 2k + 360 + t, t in [-28, 28]
+        # u3[m0 - 128 + k], k in [0, 2304): z2 local 2k + 304 + t, t in [-28, 28]
         h = (len(g2) - 1) // 2
-        u3 = np.array([np.dot(g2, z2[2 * k + 360 - h:2 * k + 361 + h]) for k in range(64 * AP_BLK)], dt)
-        V = u3.reshape(64, AP_BLK)
-        for tab in AP_TABS:
-            V = block_section(V, tab, dt=dt)
-        V = V[::-1, ::-1].copy()
-        for tab in AP_TABS:
-            V = block_section(V, tab, dt=dt)
-        v = V[::-1, ::-1].reshape(-1)
+        c0 = K2_LEFT - 2 * U3_BASE
+        u3 = np.array([np.dot(g2, z2[2 * k + c0 - h:2 * k + c0 + h + 1]) for k in range(2304)], dt)
+        v = np.zeros(K2_M, dt)
+        for q in range(4):     # wave q: outputs [512 q, + 512) from u3 [32 + 512 q, + 704)
+            k0 = U3_BASE - AP_HALO + (K2_M // 4) * q
+            V = u3[k0:k0 + 64 * AP_BLK].reshape(64, AP_BLK)
+            for tab in AP_TABS:
+                V = block_section(V, tab, dt=dt)
+            V = V[::-1, ::-1].copy()
+            for tab in AP_TABS:
+                V = block_section(V, tab, dt=dt)
+            V = V[::-1, ::-1].reshape(-1)
+            v[(K2_M // 4) * q:(K2_M // 4) * (q + 1)] = V[AP_HALO:AP_HALO + K2_M // 4]
         n = min(K2_M, n3 - m0)
-        out[m0:m0 + n] = v[AP_HALO:AP_HALO + n]
+        out[m0:m0 + n] = v[:n]
     return out
 
 
