@@ -12,7 +12,7 @@
 // block from a zero state, the exit states are combined by a Kogge-Stone scan over lanes
 // (depth from the block decay, pc_own_levels / pc_ap_levels), and each output gets the
 // entering state's response ct[t] . s (t < its decay length).  K2 tiles carry warm-up halos
-// (own rate 330 samples, output rate 80) instead of state across tiles, so every tile and
+// (own rate 276 / 438 samples, output rate 64) instead of state across tiles, so every tile and
 // every K1 tile is independent.
 // Intermediates: only y2 (rate 1/4, 8 B per 4 input samples) goes through device memory.
 #include "zfft_device.h"
@@ -201,14 +201,16 @@ __global__ void __launch_bounds__(256) pc_fir_kernel(InDesc in, const v2f *lo, v
 template <bool UP>
 __device__ __forceinline__ v2f wshift(v2f v) {
   constexpr int ctrl = UP ? 0x138 : 0x130;
-  return v2f{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.x), ctrl, 0xF, 0xF, false)),
-             __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.y), ctrl, 0xF, 0xF, false))};
+  return v2f{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.x), ctrl, 0xF, 0xF, true)),
+             __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.y), ctrl, 0xF, 0xF, true))};
 }
-template <bool UP, int N>
-__device__ __forceinline__ v2f wshiftn(v2f v) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) v = wshift<UP>(v);
-  return v;
+// Shift by SH >= 2 lanes (0 where there is no source) through ds_bpermute: the LDS crossbar
+// instead of SH dependent DPP moves on the VALU.
+template <bool UP, int SH>
+__device__ __forceinline__ v2f shiftk(v2f v, int lane) {
+  const v2f r = UP ? v2f{__shfl_up(v.x, SH, 64), __shfl_up(v.y, SH, 64)}
+                   : v2f{__shfl_down(v.x, SH, 64), __shfl_down(v.y, SH, 64)};
+  return (UP ? lane < SH : lane >= 64 - SH) ? splat(0.f) : r;
 }
 
 // One all-pole section over this lane's block v[0..B) in time order (UP) or reversed (!UP),
@@ -235,10 +237,10 @@ __device__ __forceinline__ void sec_block(v2f (&v)[B], CT tab0, LP scr, int lane
 #pragma unroll
   for (int d = 0; d < LEV; ++d) {
     v2f p0, p1;
-    if (d == 0) p0 = wshiftn<UP, 1>(e0), p1 = wshiftn<UP, 1>(e1);
-    else if (d == 1) p0 = wshiftn<UP, 2>(e0), p1 = wshiftn<UP, 2>(e1);
-    else if (d == 2) p0 = wshiftn<UP, 4>(e0), p1 = wshiftn<UP, 4>(e1);
-    else p0 = wshiftn<UP, 8>(e0), p1 = wshiftn<UP, 8>(e1);
+    if (d == 0) p0 = wshift<UP>(e0), p1 = wshift<UP>(e1);
+    else if (d == 1) p0 = shiftk<UP, 2>(e0, lane), p1 = shiftk<UP, 2>(e1, lane);
+    else if (d == 2) p0 = shiftk<UP, 4>(e0, lane), p1 = shiftk<UP, 4>(e1, lane);
+    else p0 = shiftk<UP, 8>(e0, lane), p1 = shiftk<UP, 8>(e1, lane);
     const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
     e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
     e0 = n0;
@@ -345,8 +347,8 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
 #pragma unroll
   for (int r = 0; r < 9; ++r) sp[9 * t + r] = u[r];
   __syncthreads();
-  // output-rate sections: wave q takes outputs [512 q, + 512) with 96-sample halos, u3
-  // index k = 32 + 512 q + 11 lane + i
+  // output-rate sections: wave q takes outputs [512 q, + 512) with 64-sample halos, u3
+  // index k = 64 + 512 q + 10 lane + i
   {
     v2f a[kPcApBlk];
     const int k0 = kU3Base - kPcApHalo + (kPcK2M / 4) * wave + kPcApBlk * lane;
@@ -372,13 +374,6 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
 
 // ---------------------------------------------------------------------------------- KW
 
-// a shift by 16 lanes toward higher (UP) / lower lanes, 0 where there is no source
-template <bool UP>
-__device__ __forceinline__ v2f shift16(v2f v, int lane) {
-  const v2f r = UP ? shup(v, 16) : shdn(v, 16);
-  return (UP ? lane < 16 : lane >= 48) ? splat(0.f) : r;
-}
-
 // sec_block for KW: own-rate section SI (causal: table wf, B = 16; anticausal: wb, B = 20)
 // over the 4 waves' lane blocks, the waves continuing each other; the first wave in time
 // order enters with (c0, c1): the state carried from the previous tile (causal) or 0.
@@ -400,11 +395,11 @@ __device__ __forceinline__ void wsec(v2f (&v)[B], CT tab0, LP scr, int lane, int
 #pragma unroll
   for (int d = 0; d < LEV; ++d) {
     v2f p0, p1;
-    if (d == 0) p0 = wshiftn<UP, 1>(e0), p1 = wshiftn<UP, 1>(e1);
-    else if (d == 1) p0 = wshiftn<UP, 2>(e0), p1 = wshiftn<UP, 2>(e1);
-    else if (d == 2) p0 = wshiftn<UP, 4>(e0), p1 = wshiftn<UP, 4>(e1);
-    else if (d == 3) p0 = wshiftn<UP, 8>(e0), p1 = wshiftn<UP, 8>(e1);
-    else p0 = shift16<UP>(e0, lane), p1 = shift16<UP>(e1, lane);
+    if (d == 0) p0 = wshift<UP>(e0), p1 = wshift<UP>(e1);
+    else if (d == 1) p0 = shiftk<UP, 2>(e0, lane), p1 = shiftk<UP, 2>(e1, lane);
+    else if (d == 2) p0 = shiftk<UP, 4>(e0, lane), p1 = shiftk<UP, 4>(e1, lane);
+    else if (d == 3) p0 = shiftk<UP, 8>(e0, lane), p1 = shiftk<UP, 8>(e1, lane);
+    else p0 = shiftk<UP, 16>(e0, lane), p1 = shiftk<UP, 16>(e1, lane);
     const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
     e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
     e0 = n0;

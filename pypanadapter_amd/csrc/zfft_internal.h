@@ -150,8 +150,9 @@ constexpr int kPcK2M = 2048;              // outputs per K2 tile
 constexpr int kPcK2Span = 5376;           // y2 samples per K2 tile: 256 thread blocks of 21
 constexpr int kPcK2Left = 560;            // span starts at 2 m0 - 560
 constexpr int kPcOwnBlk = 21;             // own-rate samples per thread
-constexpr int kPcApBlk = 11;              // output-rate samples per lane (each wave a quarter)
-constexpr int kPcApHalo = 96;             // output-rate warm-up per wave (0.765^96 < 1e-11)
+constexpr int kPcApBlk = 10;              // output-rate samples per lane (each wave a quarter)
+constexpr int kPcApHalo = 64;             // output-rate warm-up per wave (0.765^64 = 3.6e-8:
+                                          // the model's fp64 error 5e-8, fp32 2.5e-6 as with 96)
 constexpr int kPcG0 = 33, kPcG1 = 49, kPcG2 = 57;
 constexpr int kPcOwn = 2, kPcAp = 10;
 constexpr int kPcEdgeR = 192, kPcEdgeJ = 1536, kPcEdgeRank = 16;  // edge map capacities

@@ -20,8 +20,8 @@ Kernel structure modelled here:
   K1 tiles: 992 y2 outputs per tile from 4128 input samples (FIR alpha then beta).
   K2 tiles: 2048 outputs per tile from a 5376-sample y2 span (own-rate sections over
         256 thread blocks of 21 with block scans and cross-wave steps; FIR gamma; the
-        10-section cascade on 4 waves, each a quarter of the tile with 96-sample halos
-        over 64 lane blocks of 11), edges by the matrices.
+        10-section cascade on 4 waves, each a quarter of the tile with 64-sample halos
+        over 64 lane blocks of 10), edges by the matrices.
   (KW, the walk kernel, runs the same arithmetic with tiles in frame order: the causal
   own-rate sections carry state instead of the left halo -- same values to fp32 rounding.)
 """
@@ -133,8 +133,8 @@ K1_Q = 992         # y2 outputs per K1 tile
 K2_M = 2048        # outputs per K2 tile
 K2_SPAN = 5376     # y2 samples per K2 tile (256 x 21)
 K2_LEFT = 560      # span starts at 2 m0 - K2_LEFT
-AP_HALO = 96
-AP_BLK = 11
+AP_HALO = 64
+AP_BLK = 10
 U3_BASE = 128      # u3 index k <-> output m0 - 128 + k
 
 
