@@ -435,6 +435,13 @@ __device__ __forceinline__ void wsec(v2f (&v)[B], CT tab0, LP scr, int lane, int
 }
 
 constexpr int kWZ = 256 * kPcWb;  // own-rate samples held: span s in [256, 5376)
+// Until the anticausal pass reads them, the own-rate samples sit in a padded layout, one
+// 16-B pad after every 32 (i -> i + 2 (i / 32)): the causal pass's lane blocks of 16 are
+// 128 B apart, 8-way conflicts on every ds_read_b128 / ds_write_b128 of the plain layout and
+// none in this one.  The anticausal pass writes its outputs back in the plain layout, which
+// FIR gamma reads.
+constexpr int kWZP = kWZ + 2 * (kWZ / 32);
+__device__ __forceinline__ int zp(int i) { return i + ((i >> 5) << 1); }
 static_assert(kWZ == kPcK2Span - 256 && 256 * kPcWf == 4 * kPcWQ, "KW geometry");
 static_assert(kOutOff + kPcK2M <= kXRows * kXRow, "KW: u3 + outputs fit the input tile's LDS");
 
@@ -448,7 +455,7 @@ static_assert(kOutOff + kPcK2M <= kXRows * kXRow, "KW: u3 + outputs fit the inpu
 template <int DT, int FLIP>
 __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, CT tab) {
   __shared__ v4f xl4[kXRows * kXRow / 2];  // K1 input tile, then y1; then u3 + staged outputs
-  __shared__ v4f z4[kWZ / 2];              // own-rate samples, span s in [256, 5376)
+  __shared__ v4f z4[kWZP / 2];             // own-rate samples, span s in [256, 5376)
   __shared__ v4f scr4[16];                 // cross-wave states (4 section calls)
   __shared__ v4f car4[2];                  // causal sections' carried states
   __shared__ v4f y1c4[24];                 // the 48 y1 two sub-tiles share
@@ -457,7 +464,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
   const int64_t f = blockIdx.x, L = in.len;
   const v2f *lor = lo_row(lo, in, f);
   const v4f lane_lo = *(const v4f *)(lor + 2 * t) * (float)M_SQRT1_2;
-  for (int i = t; i < kPcWQ; i += 256) zl[i] = splat(0.f);
+  for (int i = t; i < kPcWQ; i += 256) zl[zp(i)] = splat(0.f);
   if (t < 24) y1c4[t] = v4f{0.f, 0.f, 0.f, 0.f};
   if (t < 2) car4[t] = v4f{0.f, 0.f, 0.f, 0.f};
   const int ntiles = (int)((n3 - kPcWM0 + kPcWM - 1) / kPcWM);
@@ -543,7 +550,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
             if (u + 1 >= 0 && u + 1 < kPcG1) b[r] = vfma(splat(tab->g1[u + 1]), x1, b[r]);
           }
         }
-        const LP zo = zl + kPcWQ * (1 + c) + 4 * t;
+        const LP zo = zl + zp(kPcWQ * (1 + c) + 4 * t);
         *(LP4)zo = cat(b[0], b[1]);
         *(LP4)(zo + 2) = cat(b[2], b[3]);
         if (t < 24) y1c4[t] = *(LP4)(yl + (256 + (t >> 2)) * kYRow + 2 * (t & 3));  // i = 2048 + 2 t
@@ -553,7 +560,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
     // ---- own-rate sections, causal, on the new 4096 (carried states)
     {
       v2f v[kPcWf];
-      const LP zb = zl + kPcWQ + kPcWf * t;
+      const LP zb = zl + zp(kPcWQ + kPcWf * t);  // a block of 16 never straddles a pad
 #pragma unroll
       for (int k = 0; k < kPcWf; ++k) v[k] = zb[k];
       if constexpr (!(kKo & 1)) {
@@ -576,14 +583,18 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
     // the next tile's lower 1024 causal outputs (s in [4352, 5376) -> [256, 1280))
     v2f cz[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cz[r] = zl[4 * kPcWQ + 4 * t + r];
+    for (int r = 0; r < 4; ++r) cz[r] = zl[zp(4 * kPcWQ + 4 * t) + r];
     // ---- own-rate sections, anticausal, on s in [256, 5376)
     {
       v2f v[kPcWb];
-      const LP zb = zl + kPcWb * t;
 #pragma unroll
-      for (int k = 0; k < kPcWb; ++k) v[k] = zb[k];
-      __syncthreads();  // cz read before anything is written back
+      for (int k = 0; k < kPcWb; k += 2) {  // padded layout (pairs never straddle a pad)
+        const v4f w = *(LP4)(zl + zp(kPcWb * t + k));
+        v[k] = lo2(w);
+        v[k + 1] = hi2(w);
+      }
+      const LP zb = zl + kPcWb * t;  // written back in the plain layout
+      __syncthreads();  // cz and every block read before anything is written back
       if constexpr (!(kKo & 1)) {
         wsec<kPcWb, pc_wb_levels(0), false, 0>(v, tab, scr + 16, lane, wave, splat(0.f), splat(0.f));
         wsec<kPcWb, pc_wb_levels(1), false, 1>(v, tab, scr + 24, lane, wave, splat(0.f), splat(0.f));
@@ -615,7 +626,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) zl[4 * t + r] = cz[r];
+    for (int r = 0; r < 4; ++r) zl[zp(4 * t) + r] = cz[r];
     // ---- output-rate sections (K2's: wave q takes outputs [512 q, + 512) with halos)
     {
       v2f a[kPcApBlk];
