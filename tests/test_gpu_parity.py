@@ -404,15 +404,17 @@ def test_facade_matches_reference_rows():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("z,F,L,want", [(8, 1, 299008, "pc"), (8, 384, 299008, "pc"),
-                                        (8, 768, 1048576, "pc"), (8, 4, 8192, "exact"),
+                                        (8, 768, 1048576, "pc"), (8, 4096, 32768, "walk"),
+                                        (8, 4095, 32768, "pc"), (8, 4, 8192, "exact"),
                                         (4, 1, 262144, "exact"), (4, 256, 262144, "exact"),
                                         (4, 384, 262144, "xa"), (4, 64, 1048576, "exact"),
                                         (4, 128, 1048576, "fused"), (4, 768, 1048576, "xa")])
 def test_auto_schedule_by_batch(z, F, L, want):
     """The automatic decimator schedule follows the measured crossovers (zfft_plan.cpp
-    pc_fits / auto_xa / use_fused, tools/sweep_schedule.py, profiles/r04e): at zoom 8 the PC
-    polyphase cascade for every batch of frames >= 16384 samples (one frame per call -- the
-    reference's use -- included); elsewhere small batches run the exact blocked passes,
+    pc_fits / kPcWalkMinFrames / auto_xa / use_fused, tools/sweep_schedule.py,
+    profiles/r04l): at zoom 8 the PC polyphase cascade for every batch of frames >= 16384
+    samples (one frame per call -- the reference's use -- included), as its walk kernel
+    from 4096 frames per call; elsewhere small batches run the exact blocked passes,
     batches of >= 2^27 samples the fused interior with edge windows, and >= 384 frames of
     <= 2^19 samples (768 of longer ones) the XA tiles."""
     import torch
@@ -428,7 +430,7 @@ def test_auto_schedule_by_batch(z, F, L, want):
         torch.cuda.synchronize()
         names = plan.launch_names()
     first = {"exact": ("exact_forward_mix",), "fused": ("exact_forward_mix",),
-             "xa": ("xa_stage_mix",), "pc": ("pc_fir",)}[want]
+             "xa": ("xa_stage_mix",), "pc": ("pc_fir",), "walk": ("pc_walk",)}[want]
     assert names[0] in first, names
     assert ("edge_windows" in names) == (want == "fused"), names
     del x, rows
