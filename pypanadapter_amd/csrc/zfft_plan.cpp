@@ -779,10 +779,11 @@ int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t
 // maps do not meet (kPcMinL), grid y = frames.
 constexpr int64_t kPcMinL = 16384;
 // KW (one workgroup per frame) from this many frames per call; below, K1 + K2's tiles.
-// tools/sweep_schedule.py (profiles/r04l/sweep_schedule.json, KW / tiles time per call,
-// 299,008-sample frames): 64 frames 3.37, 512 1.03, 1024 1.04, 2048 1.02, 4096 0.987
-// (2^20-sample frames 2048: 1.02): one workgroup per frame needs >= 8 rounds of the chip's
-// 512 resident workgroups to fill it; KW also keeps y2 (2 B per input sample) off HBM.
+// tools/sweep_schedule.py (KW / tiles time per call, 299,008-sample frames): 64 frames 3.2,
+// 512 1.00, 2048 0.99, 4096 1.01 (profiles/r04r; r04l: 0.987), and 0.96 on bench.py's
+// steady-state clock at 4096 (profiles/r04p): one workgroup per frame needs several rounds of
+// the chip's 512 resident workgroups to fill it; KW also keeps y2 (2 B per input sample,
+// 6 GB per cfg2 step with its read-back) off HBM.
 constexpr int kPcWalkMinFrames = 4096;
 bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == kPcStages && L >= kPcMinL && frames <= 65535;
