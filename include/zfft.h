@@ -192,8 +192,8 @@ int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *coun
 /* Comma-separated names of the intervals zfft_plan_timings returns (owned by the plan). */
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
-/* Decimator schedule: 0 = automatic -- 4 for zoom 8 and frames of >= 16384 samples (every
- * batch size); otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
+/* Decimator schedule: 0 = automatic -- for zoom 8 and frames of >= 16384 samples 4 below
+ * 4096 frames per call and 5 from there; otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
  * samples, else 2 for batches of >= 2^27 samples whose frames are long enough for the edge
  * windows, else 1 -- e.g. one frame per call, the reference's use.  Each batch of a
  * zfft_process call is judged by its own frame count; crossovers measured by
@@ -204,7 +204,9 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * each stage is one launch whose decimated output -- n_k/2 complex64 per frame -- is the next
  * stage's input in device memory), 4 = PC polyphase cascade (zoom 8 only: FIRs at falling
  * rates + the slow poles as zero-phase sections at rates 1/4 and 1/8, two launches, plus
- * rank-~10 frame-end maps; frames >= 16384 samples, <= 65535 frames per launch).  Path 3
+ * rank-~10 frame-end maps; frames >= 16384 samples, <= 65535 frames per launch), 5 = the
+ * same arithmetic as one launch with one workgroup per frame (the rate-1/4 intermediate
+ * stays on chip; automatic from 4096 frames per call).  Path 3
  * needs every stage array below 2^31 bytes per frame; a forced path outside its domain
  * returns ZFFT_EUNSUPPORTED.  All produce the reference's rows within the fp32 parity gate
  * (zfft_plan.cpp auto_xa, use_fused, pc_fits). */

@@ -119,7 +119,8 @@ class ZoomFFT:
         e.g. one frame per call), 2 fused interior + exact edges (blocked; auto from 2^27
         samples per call), 3 XA tiles (all-pole + FIR + half-rate all-pole, one wave per
         frame; auto for >= 768 frames, or >= 384 frames of <= 2^19 samples), 4 PC polyphase
-        cascade (zoom 8, frames >= 16384 samples; the auto choice there at every batch)."""
+        cascade tiles (zoom 8, frames >= 16384 samples; the auto choice there below 4096
+        frames per call), 5 the PC walk (one workgroup per frame; auto from 4096 frames)."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
 
     def set_welch(self, mode: int) -> None:

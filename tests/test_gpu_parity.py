@@ -553,11 +553,11 @@ def test_lo_rows_refused_at_zoom_1():
         plan.set_lo_frames([], 1)
 
 
-@pytest.mark.parametrize("path,first", [(0, "pc_fir"), (3, "xa_stage_mix")])
+@pytest.mark.parametrize("path,first", [(0, "pc_walk"), (4, "pc_fir"), (3, "xa_stage_mix")])
 def test_lo_per_frame_bench_batch(oracle_lib, path, first):
     """Config 4 at the bench's geometry: 8 IFs x 512 frames of cfg2 in one F = 4096 batch on
-    the device (the automatic schedule, PC, and XA), two frames of every IF vs the oracle at
-    that IF's f_LO."""
+    the device (the automatic schedule -- the PC walk at this batch --, the PC tiles and XA),
+    two frames of every IF vs the oracle at that IF's f_LO."""
     import torch
     import bench
     from pypanadapter_amd import ZoomFFT

@@ -1,3 +1,3 @@
 set -u
 export TMPDIR=/tmp
-bash tools/gpu_session.sh r04s tests
+bash tools/gpu_session.sh r04t tests smoke
