@@ -1,3 +1,6 @@
+# Scratch GPU command of the last session (run as: gpurun -- 'bash tools/_cmd.sh'):
+# the final-hash stamp session, then the scheduler-strategy A/B (variants from
+# tools/build_variants.py).
 set -u
 export TMPDIR=/tmp
 V=pypanadapter_amd/lib/variants
