@@ -1,6 +1,6 @@
 # Scratch GPU command of the last session (run as: gpurun -- 'bash tools/_cmd.sh'):
-# the final confirmation at the round's last commit: GPU parity suite, smoke, the driver's
-# own bench line.
+# K3 rewritten with one wave per frame and side (not kept): GPU parity suite and a
+# quick bench for its time.
 set -u
 export TMPDIR=/tmp
-bash tools/gpu_session.sh r04w tests smoke driver
+bash tools/gpu_session.sh r04x tests quick
