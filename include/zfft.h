@@ -39,6 +39,7 @@ extern "C" {
 #define ZFFT_ENOMEM (-4)       /* device or host allocation failed                       */
 #define ZFFT_ENODEV (-5)       /* no HIP device                                          */
 #define ZFFT_EUNSUPPORTED (-6) /* valid in the reference but not built in this version   */
+#define ZFFT_EINTERNAL (-7)    /* the library's own filter tables failed a consistency check */
 
 /* window kinds: scipy.signal.get_window(kind, M) with fftbins=True (periodic), the taper
  * list of FFTTaperingControl (pypanadapter_spectrum.py:1222-1243) */
@@ -196,8 +197,12 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * 4096 frames per call and 5 from there; otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
  * samples, else 2 for batches of >= 2^27 samples whose frames are long enough for the edge
  * windows, else 1 -- e.g. one frame per call, the reference's use.  Each batch of a
- * zfft_process call is judged by its own frame count; crossovers measured by
- * tools/sweep_schedule.py (profiles/r04e/sweep_schedule.json).
+ * zfft_process call is judged by its own frame count (host calls are split into batches of
+ * about 1 GiB of input -- 418 cfg2 frames -- so from host memory path 5 is reached only by
+ * forcing it; zfft_process_device judges the whole call); crossovers measured by
+ * tools/sweep_schedule.py (profiles/r04v/sweep_schedule.json).  Default tolerance: the
+ * automatic zoom-8 choice (PC, paths 4/5, also for one frame per call) gives the float64
+ * reference's decimated IQ within 5e-6 of its peak (measured 2-3e-6; path 1: 2e-6).
  * 1 = blocked warm-up passes in the reference order (frames split over many waves),
  * 2 = blocked, fused commuted-order interior + exact edge windows, 3 = XA tiles (one wave per
  * frame and stage: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned;

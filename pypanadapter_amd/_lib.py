@@ -19,6 +19,7 @@ ZFFT_EHIP = -3
 ZFFT_ENOMEM = -4
 ZFFT_ENODEV = -5
 ZFFT_EUNSUPPORTED = -6
+ZFFT_EINTERNAL = -7
 
 WINDOW_KINDS = {
     "hamming": 0, "hann": 1, "blackman": 2, "blackmanharris": 3, "nuttall": 4, "flattop": 5,

@@ -39,16 +39,27 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH,
     passed to hipcc as it is (e.g. "-mllvm", "-amdgpu-sched-strategy=max-ilp")."""
     if not force and not defines and out == LIB_PATH and not needs_build():
         return LIB_PATH
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     tmp = out + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
-    cmd += [d if d.startswith("-") else f"-D{d}" for d in defines]
-    cmd += [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+             "-Wall", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    flags += [d if d.startswith("-") else f"-D{d}" for d in defines]
+    with tempfile.TemporaryDirectory(prefix="zfft_build_") as td:
+        # one object per source, compiled in parallel (the kernel files dominate), then linked
+        def obj(s):
+            o = os.path.join(td, s + ".o")
+            cmd = [hipcc, *flags, "-c", os.path.join(CSRC, s), "-o", o]
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.run(cmd, check=True)
+            return o
+        with ThreadPoolExecutor(min(len(SOURCES), os.cpu_count() or 1)) as ex:
+            objs = list(ex.map(obj, SOURCES))
+        subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp],
+                       check=True)
     os.replace(tmp, out)
     if out == LIB_PATH:  # a knob build there is recorded as such: the next build() replaces it
         _write_build_info(defines)

@@ -28,9 +28,33 @@ constexpr int kKo = PC_KO;
 #else
 constexpr int kKo = 0;
 #endif
+// PC_STAMPS=1 (diagnostic builds only): per-phase s_memtime sums of every walk wave, read back
+// with zfft_debug_pc_stamps (tools/pc_stamps.py); no stamp exists otherwise.
+#if !ZFFT_DIAG && defined(PC_STAMPS)
+#error "PC_STAMPS is a diagnostic knob: build with -DZFFT_DIAG"
+#endif
+#ifndef PC_STAMPS
+#define PC_STAMPS 0
+#endif
 
 namespace zfft {
 namespace pc {
+
+[[maybe_unused]] constexpr int kPcStampSegs = 9;
+#if PC_STAMPS
+__device__ unsigned long long g_pc_stamps[kPcStampSegs + 1];
+#define PC_STAMP(i)                                                                   \
+  {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    unsigned long long t_;                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    st_acc[i] += t_ - t_prev;                                                         \
+    t_prev = t_;                                                                      \
+  }
+#else
+#define PC_STAMP(i)
+#endif
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef v2f __attribute__((address_space(3))) *LP;
@@ -68,19 +92,35 @@ __device__ __forceinline__ int xidx(int s) { return (s >> 4) * kXRow + (s & 15);
 // prefetch) and its conversion to complex64
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef unsigned char u8x4 __attribute__((ext_vector_type(4)));
+// T: the pair as a value; U: the same type aligned only to one element, the alignment the
+// address has (the first sample of a pair is any sample: odd L, flip).  The U loads still
+// compile to one global_load_dwordx4 / dwordx2 / dword / short: gfx950 global loads need no
+// natural alignment (unaligned access mode), and the type says so instead of relying on it.
 template <int DT> struct RawP;
-template <> struct RawP<kInC64> { typedef v4f T; };
-template <> struct RawP<kInC32H> { typedef h4 T; };
-template <> struct RawP<kInF32R> { typedef float2 T; };
-template <> struct RawP<kInCU8> { typedef u8x4 T; };
+template <> struct RawP<kInC64> {
+  typedef v4f T;
+  typedef float U __attribute__((ext_vector_type(4), aligned(8)));
+};
+template <> struct RawP<kInC32H> {
+  typedef h4 T;
+  typedef _Float16 U __attribute__((ext_vector_type(4), aligned(4)));
+};
+template <> struct RawP<kInF32R> {
+  typedef v2f T;
+  typedef float U __attribute__((ext_vector_type(2), aligned(4)));
+};
+template <> struct RawP<kInCU8> {
+  typedef u8x4 T;
+  typedef unsigned char U __attribute__((ext_vector_type(4), aligned(2)));
+};
 template <int DT, int FLIP>
 __device__ __forceinline__ typename RawP<DT>::T raw_pair(const InDesc &in, int64_t f, int64_t n) {
-  typedef typename RawP<DT>::T T;
+  typedef const typename RawP<DT>::U *UP;
   const int64_t k = f * in.stride + (FLIP ? in.len - 2 - n : n);  // first raw element
-  if constexpr (DT == kInC64) return *(const T *)((const v2f *)in.p + k);
-  else if constexpr (DT == kInC32H) return *(const T *)((const h2 *)in.p + k);
-  else if constexpr (DT == kInF32R) return *(const T *)((const float *)in.p + k);
-  else return *(const T *)((const u8x2 *)in.p + k);
+  if constexpr (DT == kInC64) return *(UP)((const v2f *)in.p + k);
+  else if constexpr (DT == kInC32H) return *(UP)((const h2 *)in.p + k);
+  else if constexpr (DT == kInF32R) return *(UP)((const float *)in.p + k);
+  else return *(UP)((const u8x2 *)in.p + k);
 }
 template <int DT, int FLIP>
 __device__ __forceinline__ void cvt_pair(typename RawP<DT>::T w, v2f &a, v2f &b) {
@@ -482,6 +522,10 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
     }
   };
   prefetch(0);
+#if PC_STAMPS
+  unsigned long long st_acc[kPcStampSegs] = {}, t_prev;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_prev)::"memory");
+#endif
   for (int tau = 0; tau < ntiles; ++tau) {
     const int64_t m0 = kPcWM0 + (int64_t)kPcWM * tau;
     // ---- FIRs: y2 for s in [1280, 5376), four sub-tiles
@@ -508,6 +552,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
         prefetch(4 * tau + c + 1);
       }
       __syncthreads();
+      PC_STAMP(0);
       v2f acc[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) acc[r] = splat(0.f);
@@ -527,12 +572,14 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
         }
       }
       __syncthreads();
+      PC_STAMP(1);
       // y1 local i <-> 2 Q - 24 + i: [0, 48) carried, thread t's 8 at 48 + 8 t (row 6 + t)
       const LP yl = xl;
       if (t < 24) *(LP4)(yl + (t >> 2) * kYRow + 2 * (t & 3)) = y1c4[t];
 #pragma unroll
       for (int q = 0; q < 4; ++q) *(LP4)(yl + (6 + t) * kYRow + 2 * q) = cat(acc[2 * q], acc[2 * q + 1]);
       __syncthreads();
+      PC_STAMP(2);
       {
         v2f b[4];
 #pragma unroll
@@ -556,6 +603,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
         if (t < 24) y1c4[t] = *(LP4)(yl + (256 + (t >> 2)) * kYRow + 2 * (t & 3));  // i = 2048 + 2 t
       }
       __syncthreads();
+      PC_STAMP(3);
     }
     // ---- own-rate sections, causal, on the new 4096 (carried states)
     {
@@ -580,6 +628,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
       for (int k = 0; k < kPcWf; ++k) zb[k] = v[k];
     }
     __syncthreads();
+    PC_STAMP(4);
     // the next tile's lower 1024 causal outputs (s in [4352, 5376) -> [256, 1280))
     v2f cz[4];
 #pragma unroll
@@ -603,6 +652,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
       for (int k = 0; k < kPcWb; ++k) zb[k] = v[k];
     }
     __syncthreads();
+    PC_STAMP(5);
     // ---- FIR gamma (K2's): u3 index k = 9 t + r (output m0 - 128 + k) from z s in [2k + 276, + 56]
     {
       v2f u[9];
@@ -625,6 +675,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
       for (int r = 0; r < 9; ++r) xl[9 * t + r] = u[r];
     }
     __syncthreads();
+    PC_STAMP(6);
 #pragma unroll
     for (int r = 0; r < 4; ++r) zl[zp(4 * t) + r] = cz[r];
     // ---- output-rate sections (K2's: wave q takes outputs [512 q, + 512) with halos)
@@ -637,6 +688,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
         ap_cascade<0, true>(a, tab, lane);
         ap_cascade<0, false>(a, tab, lane);
       }
+      PC_STAMP(7);
 #pragma unroll
       for (int i = 0; i < kPcApBlk; ++i) {
         const int k = k0 + i - kU3Base;
@@ -651,7 +703,15 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
       if (m >= 0 && m < n3) ob[m] = xl[kOutOff + s];
     }
     __syncthreads();
+    PC_STAMP(8);
   }
+#if PC_STAMPS
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < kPcStampSegs; ++i) atomicAdd(&g_pc_stamps[i], st_acc[i]);
+    atomicAdd(&g_pc_stamps[kPcStampSegs], (unsigned long long)ntiles);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------- K3
@@ -699,6 +759,19 @@ __global__ void __launch_bounds__(256) pc_edge_kernel(InDesc in, const v2f *lo, 
 }
 
 }  // namespace pc
+
+// Debug hook (not part of zfft.h): copies and clears the walk's stamp sums of a PC_STAMPS build
+// (segment cycles summed over waves, then the tile count summed over workgroups); -1 otherwise.
+extern "C" int zfft_debug_pc_stamps(unsigned long long *out) {
+#if PC_STAMPS
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pc::g_pc_stamps), sizeof(pc::g_pc_stamps)) != hipSuccess) return -2;
+  unsigned long long z[pc::kPcStampSegs + 1] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(pc::g_pc_stamps), z, sizeof(z)) == hipSuccess ? 0 : -2;
+#else
+  (void)out;
+  return -1;
+#endif
+}
 
 #define PC_LAUNCH2(KERNEL, DT, fl, ...)                                                         \
   do {                                                                                           \

@@ -19,10 +19,12 @@
 #include <cmath>
 #include <complex>
 #include <cstring>
+#include <system_error>
 #include <thread>
 #include <vector>
 
 #include "cheby1_q2.h"
+#include "pc_edge_maps.h"
 #include "zfft_internal.h"
 
 namespace zfft {
@@ -239,23 +241,29 @@ void edge_matrix(int side, int lmod8, int R, int J, std::vector<double> &C) {
   const std::vector<double> &hz = model_hz();
   C.assign((size_t)R * J, 0.0);
   const int nt = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
-  std::vector<std::thread> pool;
-  for (int w = 0; w < nt; ++w)
-    pool.emplace_back([&, w] {
-      std::vector<double> x(Lc), out;
-      for (int j = w; j < J; j += nt) {
-        const int pos = side == 0 ? j : Lc - 1 - j;
-        std::fill(x.begin(), x.end(), 0.0);
-        x[pos] = 1.0;
-        exact3(x, out);
-        for (int m = 0; m < R; ++m) {
-          const int mo = side == 0 ? m : n3 - 1 - m;
-          const long n = 8L * mo - pos;
-          const double model = (n >= -kHz && n <= kHz) ? hz[n + kHz] : 0.0;
-          C[(size_t)m * J + j] = out[mo] - model;
-        }
+  auto work = [&](int w) {
+    std::vector<double> x(Lc), out;
+    for (int j = w; j < J; j += nt) {
+      const int pos = side == 0 ? j : Lc - 1 - j;
+      std::fill(x.begin(), x.end(), 0.0);
+      x[pos] = 1.0;
+      exact3(x, out);
+      for (int m = 0; m < R; ++m) {
+        const int mo = side == 0 ? m : n3 - 1 - m;
+        const long n = 8L * mo - pos;
+        const double model = (n >= -kHz && n <= kHz) ? hz[n + kHz] : 0.0;
+        C[(size_t)m * J + j] = out[mo] - model;
       }
-    });
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int w = 0; w < nt; ++w) {
+    try {
+      pool.emplace_back(work, w);
+    } catch (const std::system_error &) {  // no thread: this share on the calling thread
+      work(w);
+    }
+  }
   for (auto &t : pool) t.join();
 }
 
@@ -392,7 +400,8 @@ bool pc_edge_map(int side, int lmod8, PcEdge &out) {
 
 // Test hook (not part of include/zfft.h): the PC tables, for the CPU suite.
 //   what 0: FIR taps g0 | g1 | g2 (139 floats); 1: PcTab as raw floats;
-//   2 / 3: left / right edge map for L mod 8 = arg: R, J, r then U (R x r), V (J x r).
+//   2 / 3: left / right edge map for L mod 8 = arg built now (fp64): R, J, r then U (R x r), V (J x r);
+//   4: the shipped constant map arg of pc_edge_maps.h: R, J, r then U (R x r), V^T (r x J).
 extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
   using namespace zfft;
   if (what == 0 || what == 1) {
@@ -411,8 +420,23 @@ extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
     std::memcpy(out, &t, sizeof(t));
     return n;
   }
+  if (what == 4) {  // the shipped constant map arg (0 start, 1 + k end for L mod 8 = k)
+    if (arg < 0 || arg >= kPcEdgeMaps) return -3;
+    const PcEdgeConst &m = kPcEdgeIdx[arg];
+    const int n = 3 + m.R * m.r + m.J * m.r;
+    if (cap < n) return -2;
+    out[0] = (float)m.R;
+    out[1] = (float)m.J;
+    out[2] = (float)m.r;
+    std::memcpy(out + 3, kPcEdgeData + m.u, sizeof(float) * (size_t)(m.R * m.r + m.J * m.r));
+    return n;  // U (R x r) then V^T (r x J), as stored
+  }
   PcEdge e;
-  if (!pc_edge_map(what - 2, arg & 7, e)) return -1;
+  try {  // fp64 builder (threads, large vectors): nothing may cross the C ABI
+    if (!pc_edge_map(what - 2, arg & 7, e)) return -1;
+  } catch (...) {
+    return -4;
+  }
   const int n = 3 + e.R * e.r + e.J * e.r;
   if (cap < n) return -2;
   out[0] = (float)e.R;

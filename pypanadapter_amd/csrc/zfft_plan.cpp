@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "cheby1_q2.h"
+#include "pc_edge_maps.h"
 #include "zfft.h"
 #include "zfft_internal.h"
 
@@ -404,9 +405,8 @@ struct zfft_plan {
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
   DevBuf edge, xk, xa_tab, tws, means, z4, winf;
   DevBuf pc_tab, pc_edge;  // PC decimator: PcTab; edge maps U0 V0 U1 V1 (floats)
-  int pc_lm = -1;          // L mod 8 of the right-edge map in pc_edge (-1: none)
-  int pc_R[2] = {}, pc_J[2] = {}, pc_r[2] = {};
-  size_t pc_off[4] = {};   // float offsets of U0 V0 U1 V1 in pc_edge
+                           // (pc_edge: all nine maps of pc_edge_maps.h, uploaded once)
+  int64_t n_quiesce = 0;   // host waits on enqueued work (test hook zfft__plan_quiesce_count)
   // waterfall rendering: colormap LUT (host copy + device), levels
   uint8_t lut[256 * 4] = {};
   bool lut_ready = false;         // lut holds the chosen map (built on first use)
@@ -789,8 +789,8 @@ bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == kPcStages && L >= kPcMinL && frames <= 65535;
 }
 
-// Host copies of the PC tables: built once per process (the edge maps per L mod 8, on
-// first use: ~0.2 s each).
+// Host copy of the PC tables: built once per process (fp64, microseconds); the frame-end maps
+// are the constants of pc_edge_maps.h (tools/gen_pc_edge.py).
 const PcTab *pc_host_tab() {
   static const std::unique_ptr<PcTab> t = [] {
     std::unique_ptr<PcTab> x(new PcTab());
@@ -799,49 +799,20 @@ const PcTab *pc_host_tab() {
   }();
   return t.get();
 }
-const PcEdge *pc_host_edge(int side, int lm) {
-  static std::mutex mu;
-  static std::unique_ptr<PcEdge> cache[9];  // [0..7] frame end by L mod 8, [8] frame start
-  std::lock_guard<std::mutex> lock(mu);
-  std::unique_ptr<PcEdge> &e = cache[side == 0 ? 8 : (lm & 7)];
-  if (!e) {
-    std::unique_ptr<PcEdge> x(new PcEdge());
-    if (pc_edge_map(side, lm & 7, *x)) e = std::move(x);
-  }
-  return e.get();
-}
-
-int ensure_pc(zfft_plan *p, int64_t L) {
-  if (!p->pc_tab.p) {
-    const PcTab *t = pc_host_tab();
-    if (!t) return fail(ZFFT_EHIP, "PC tables: scan depth or correction length too short");
-    hipError_t e = p->pc_tab.ensure(sizeof(PcTab));
-    if (e == hipSuccess) e = hipMemcpy(p->pc_tab.p, t, sizeof(PcTab), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(e, "PC table upload");
-  }
-  const int lm = (int)(L & 7);
-  if (p->pc_lm == lm) return ZFFT_OK;
-  const PcEdge *e0 = pc_host_edge(0, 0), *e1 = pc_host_edge(1, lm);
-  if (!e0 || !e1) return fail(ZFFT_EHIP, "PC frame-end maps: support beyond the computed block");
-  int rc = quiesce(p);  // enqueued work may still read the old maps
-  if (rc) return rc;
-  const PcEdge *es[2] = {e0, e1};
-  std::vector<float> h;
-  for (int s = 0; s < 2; ++s) {
-    p->pc_R[s] = es[s]->R;
-    p->pc_J[s] = es[s]->J;
-    p->pc_r[s] = es[s]->r;
-    p->pc_off[2 * s] = h.size();
-    h.insert(h.end(), es[s]->U.begin(), es[s]->U.end());
-    p->pc_off[2 * s + 1] = h.size();  // V transposed to r x J: lanes j read consecutive floats
-    const int J = es[s]->J, r = es[s]->r;
-    for (int k = 0; k < r; ++k)
-      for (int j = 0; j < J; ++j) h.push_back(es[s]->V[(size_t)j * r + k]);
-  }
-  hipError_t e = p->pc_edge.ensure(h.size() * sizeof(float));
-  if (e == hipSuccess) e = hipMemcpy(p->pc_edge.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "PC edge map upload");
-  p->pc_lm = lm;
+// The PC tables and all nine frame-end maps, uploaded on the plan's first PC call; nothing is
+// uploaded afterwards, so a change of L mod 8 between calls never waits on enqueued work.
+int ensure_pc(zfft_plan *p) {
+  if (p->pc_tab.p && p->pc_edge.p) return ZFFT_OK;
+  const PcTab *t = pc_host_tab();
+  if (!t) return fail(ZFFT_EINTERNAL, "PC tables: scan depth or correction length too short");
+  for (const PcEdgeConst &m : kPcEdgeIdx)
+    if (m.r > kPcEdgeRank || m.R > kPcEdgeR || m.R > 256)
+      return fail(ZFFT_EINTERNAL, "PC frame-end maps exceed the kernel's capacities");
+  hipError_t e = p->pc_tab.ensure(sizeof(PcTab));
+  if (e == hipSuccess) e = hipMemcpy(p->pc_tab.p, t, sizeof(PcTab), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = p->pc_edge.ensure(sizeof(kPcEdgeData));
+  if (e == hipSuccess) e = hipMemcpy(p->pc_edge.p, kPcEdgeData, sizeof(kPcEdgeData), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "PC table upload");
   return ZFFT_OK;
 }
 
@@ -849,7 +820,7 @@ int ensure_pc(zfft_plan *p, int64_t L) {
 // out (pong) -> K3 (frame-end maps, in place).
 int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vector<int64_t> &n,
            bool walk, const float2 **out, hipStream_t st) {
-  int rc = ensure_pc(p, L);
+  int rc = ensure_pc(p);
   if (rc) return rc;
   const int64_t n3 = n[p->K];
   const PcTab *tab = p->pc_tab.as<PcTab>();
@@ -872,11 +843,13 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
     if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
     mark(p, st, "pc_tail");
   }
+  // map 0 = frame start, 1 + (L mod 8) = frame end (pc_edge_maps.h)
   const float *eb = p->pc_edge.as<float>();
-  const float *const U[2] = {eb + p->pc_off[0], eb + p->pc_off[2]};
-  const float *const V[2] = {eb + p->pc_off[1], eb + p->pc_off[3]};
-  e = launch_pc_edge(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, U, V, p->pc_R,
-                     p->pc_J, p->pc_r, st);
+  const PcEdgeConst &m0 = kPcEdgeIdx[0], &m1 = kPcEdgeIdx[1 + (L & 7)];
+  const float *const U[2] = {eb + m0.u, eb + m1.u};
+  const float *const V[2] = {eb + m0.v, eb + m1.v};
+  const int R[2] = {m0.R, m1.R}, J[2] = {m0.J, m1.J}, r[2] = {m0.r, m1.r};
+  e = launch_pc_edge(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, U, V, R, J, r, st);
   if (e != hipSuccess) return hip_fail(e, "pc_edge launch");
   mark(p, st, "pc_edge");
   *out = p->pong.as<float2>();
@@ -1053,6 +1026,7 @@ int done_on(zfft_plan *p, hipStream_t st) {
 // overwrites a table that work may still read).
 int quiesce(zfft_plan *p) {
   if (!p->has_work) return ZFFT_OK;
+  ++p->n_quiesce;
   hipError_t e = hipEventSynchronize(p->done_ev);
   return e == hipSuccess ? ZFFT_OK : hip_fail(e, "hipEventSynchronize");
 }
@@ -1065,6 +1039,10 @@ int enter(zfft_plan *p) {
 }
 
 }  // namespace
+
+// Test hook (not part of include/zfft.h): how often the plan has waited on the host for its
+// enqueued work (a table upload that must not overwrite data in use, a synchronous call).
+extern "C" int64_t zfft__plan_quiesce_count(const zfft_plan *p) { return p ? p->n_quiesce : -1; }
 
 extern "C" {
 

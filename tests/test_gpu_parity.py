@@ -95,14 +95,15 @@ def test_zoomfft_fixtures():
         n_fft, n_avg, ratio, seed = (int(v) for v in zf[nm + "/meta"])
         ref = zf[nm + "/y"]
         # path 1 (exact sosfiltfilt order) at 2e-6; the automatic schedule too, which is the
-        # PC cascade for zoom 8 from 16384 samples on (its bound, test_gpu_pc.PC_TOL, 1e-5)
+        # PC cascade for zoom 8 from 16384 samples on: measured 2-3e-6 of the peak, held at 5e-6
+        # here (the documented default tolerance, include/zfft.h zfft_plan_path)
         for path in (1, 0):
             with ZoomFFT(max(32, n_fft), ratio, 2.4e6) as plan:
                 plan.set_path(path)
                 y = plan.decimate(zf[nm + "/x"])
             assert y.shape == ref.shape and y.dtype == np.complex64
             err = np.abs(y - ref).max() / np.abs(ref).max()
-            tol = 1e-5 if (path == 0 and ratio == 8 and zf[nm + "/x"].size >= 16384) else 2e-6
+            tol = 5e-6 if (path == 0 and ratio == 8 and zf[nm + "/x"].size >= 16384) else 2e-6
             assert err < tol, (nm, path, err)
 
 

@@ -181,3 +181,39 @@ def test_pc_size_independent_properties(path):
     np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(c, a[perm])
     np.testing.assert_allclose(d - a, 20 * np.log10(4.0), atol=2e-4)
+
+
+@PC_PATHS
+def test_pc_ragged_lengths_on_a_caller_stream(oracle_lib, zfft_lib, path):
+    """L mod 8 = 0..7 in turn through zfft_process_device on a caller stream.  Every frame-end
+    map is resident from the plan's first PC call (pc_edge_maps.h), so after a first call at
+    the longest length none of these calls waits on the host, and every
+    row passes the oracle gate."""
+    import ctypes
+    import torch
+    from pypanadapter_amd import ZoomFFT
+    count = zfft_lib.zfft__plan_quiesce_count
+    count.argtypes, count.restype = [ctypes.c_void_p], ctypes.c_int64
+    Ls = [20000 + k for k in (3, 0, 7, 1, 6, 2, 5, 4)]  # every L mod 8, shuffled
+    F, N, W = 2, 1024, 128
+    dev = torch.device("cuda:0")
+    xs = {L: _frames(F, L, N, 8, W, seed0=7700 + L) for L in Ls}
+    d_in = {L: torch.from_numpy(np.ascontiguousarray(x).view(np.float32)).to(dev) for L, x in xs.items()}
+    rows = {L: torch.empty((F, W), dtype=torch.float32, device=dev) for L in Ls}
+    st = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+    with ZoomFFT(N, 8, 2.4e6, n_win=W) as plan:
+        plan.set_path(path)
+        Lmax = max(Ls)
+        plan.process_device(d_in[Lmax].data_ptr(), Lmax, F, rows[Lmax].data_ptr(), st.cuda_stream)
+        st.synchronize()
+        q0 = count(plan._plan)
+        for L in Ls:
+            plan.process_device(d_in[L].data_ptr(), L, F, rows[L].data_ptr(), st.cuda_stream)
+        q1 = count(plan._plan)
+        st.synchronize()
+    assert q0 >= 0 and q1 == q0, (q0, q1)
+    for L in Ls:
+        got = rows[L].cpu().numpy()
+        for f in range(F):
+            assert_row_close(got[f], oracle_lib.psd_row(xs[L][f], 2.4e6, N, 8, W), f"L={L} frame {f}")

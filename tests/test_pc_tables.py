@@ -1,7 +1,8 @@
 """CPU checks of the PC decimator's host tables (pc_tables.cpp, no GPU needed):
 
 * the FIR taps equal the polyphase factorisation rebuilt here from scipy's cheby1 sections;
-* the LTI model those tables describe plus the library's frame-end maps reproduces
+* the LTI model those tables describe plus the library's shipped frame-end maps
+  (pc_edge_maps.h, equal bit for bit to the fp64 builder's) reproduces
   3 x scipy.signal.decimate(x, 2) -- the reference's zoomfft at zoom 8
   (pypanadapter_spectrum.py:2096-2098) -- in float64, for every L mod 8.
 
@@ -100,12 +101,34 @@ def test_pc_fir_taps_match_polyphase_factorisation():
         np.testing.assert_allclose(gg, gg[::-1], atol=1e-15)
 
 
-def _edge(side, lm):
+def _edge_built(side, lm):
+    """U (R x r), V (J x r) of the library's fp64 builder, run now."""
     v = _call(2 + side, lm)
     R, J, r = int(v[0]), int(v[1]), int(v[2])
-    U = v[3:3 + R * r].reshape(R, r)
-    V = v[3 + R * r:3 + R * r + J * r].reshape(J, r)
+    return v[3:3 + R * r].reshape(R, r), v[3 + R * r:3 + R * r + J * r].reshape(J, r)
+
+
+def _edge_shipped(side, lm):
+    """U, V of the constant map the plan uploads (pc_edge_maps.h, stored U then V^T)."""
+    v = _call(4, 0 if side == 0 else 1 + lm)
+    R, J, r = int(v[0]), int(v[1]), int(v[2])
+    return v[3:3 + R * r].reshape(R, r), v[3 + R * r:3 + R * r + J * r].reshape(r, J).T
+
+
+def _edge(side, lm):
+    U, V = _edge_shipped(side, lm)
     return U @ V.T
+
+
+@pytest.mark.parametrize("side,lm", [(0, 0)] + [(1, k) for k in range(8)])
+def test_shipped_edge_maps_are_the_builders(side, lm):
+    """pc_edge_maps.h (tools/gen_pc_edge.py) holds exactly what pc_edge_map builds today: the
+    constants cannot drift from the sources they were generated from."""
+    Ub, Vb = _edge_built(side, lm)
+    Us, Vs = _edge_shipped(side, lm)
+    assert Ub.shape == Us.shape and Vb.shape == Vs.shape
+    np.testing.assert_array_equal(Us, Ub)
+    np.testing.assert_array_equal(Vs, Vb)
 
 
 @pytest.mark.parametrize("L", [16384, 16385, 16386, 16387, 20004, 20005, 20006, 20007])
