@@ -175,6 +175,13 @@ int zfft_waterfall_render(zfft_plan *plan, uint8_t *rgba_out /* host, H*n_win*4 
 int zfft_waterfall_render_device(zfft_plan *plan, uint8_t *d_rgba /* H*n_win*4 */,
                                  void *hip_stream);
 
+/* Page-locked host memory (hipHostMalloc on the current device), e.g. for rgba_out: a render
+ * (or a zfft_process row block) copied into it moves at PCIe DMA rate; into pageable memory
+ * the runtime stages the copy through its own bounce buffer at a fraction of that (W = 8192:
+ * 67 MB per image).  Free with zfft_host_free. */
+int zfft_host_alloc(size_t bytes, void **out);
+int zfft_host_free(void *ptr);
+
 /* Native window generation (fp64), for tests and for callers without scipy. */
 int zfft_window_values(int32_t kind, const double *param, int32_t length, double *out);
 

@@ -1524,6 +1524,23 @@ int zfft_waterfall_render(zfft_plan *p, uint8_t *rgba_out) {
   return e == hipSuccess ? ZFFT_OK : hip_fail(e, "render copy");
 }
 
+int zfft_host_alloc(size_t bytes, void **out) {
+  if (!out || bytes == 0) return fail(ZFFT_EINVAL, "zfft_host_alloc: null output or zero size");
+  *out = nullptr;
+  hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return fail(ZFFT_ENOMEM, "page-locked host allocation failed");
+  }
+  return ZFFT_OK;
+}
+
+int zfft_host_free(void *ptr) {
+  if (!ptr) return ZFFT_OK;
+  hipError_t e = hipHostFree(ptr);
+  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "hipHostFree");
+}
+
 int zfft_waterfall_autolevel(zfft_plan *p, double *minlev, double *maxlev) {
   int rc = enter(p);
   if (rc) return rc;

@@ -264,10 +264,25 @@ class ZoomFFT:
               "zfft_waterfall_autolevel")
         return lo.value, hi.value
 
-    def waterfall_render(self) -> np.ndarray:
-        """RGBA uint8 (H, W, 4): the pixels pyqtgraph's ImageItem draws for the ring image."""
+    def waterfall_render(self, out: np.ndarray | None = None) -> np.ndarray:
+        """RGBA uint8 (H, W, 4): the pixels pyqtgraph's ImageItem draws for the ring image.
+
+        Without `out` the image lands in one of two page-locked buffers the engine owns and
+        uses in turn (the D2H copy then runs at PCIe DMA rate; a pageable array is staged
+        through the runtime's bounce buffer at a fraction of it): the returned array stays
+        valid until the render after next -- what `setImage` each line needs.  Pass `out`
+        (any C-contiguous (H, W, 4) uint8 array; page-locked from `pinned_empty` for speed)
+        to keep an image longer."""
         h, w = self.waterfall_shape()
-        out = np.empty((h, w, 4), dtype=np.uint8)
+        if out is None:
+            slots = getattr(self, "_render_slots", None)
+            if not slots or slots[0].shape != (h, w, 4):
+                slots = self._render_slots = [pinned_empty((h, w, 4), np.uint8) for _ in range(2)]
+                self._render_k = 0
+            out = slots[self._render_k % 2]
+            self._render_k += 1
+        elif out.shape != (h, w, 4) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous uint8 array of shape {(h, w, 4)}")
         check(self.lib.zfft_waterfall_render(self._plan, out.ctypes.data_as(ctypes.c_void_p)),
               "zfft_waterfall_render")
         return out
@@ -353,6 +368,33 @@ class IQRing:
         check(self.lib.zfft_ring_process(self._ring, plan._plan, row.ctypes.data_as(ctypes.c_void_p),
                                          ctypes.byref(produced)), "zfft_ring_process")
         return row[:plan.row_length] if produced.value else None
+
+
+class _PinnedBlock:
+    """One zfft_host_alloc block; arrays made by `pinned_empty` hold a reference to it."""
+
+    def __init__(self, nbytes: int):
+        self._lib = _lib.load()
+        p = ctypes.c_void_p()
+        check(self._lib.zfft_host_alloc(max(1, int(nbytes)), ctypes.byref(p)), "zfft_host_alloc")
+        self.ptr = p.value
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._lib.zfft_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def pinned_empty(shape, dtype) -> np.ndarray:
+    """An uninitialised numpy array in page-locked host memory (zfft_host_alloc), freed when
+    the last array viewing it is collected: the fast destination for D2H copies (renders,
+    rows) and source for H2D."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    blk = _PinnedBlock(n)
+    raw = (ctypes.c_char * max(1, n)).from_address(blk.ptr)
+    raw._zfft_owner = blk  # the ctypes array keeps the block alive; the ndarray keeps it
+    return np.frombuffer(raw, dtype=dt, count=int(np.prod(shape))).reshape(shape)
 
 
 def colormap_lut(name: str) -> np.ndarray:
