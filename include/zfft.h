@@ -209,7 +209,7 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * forcing it; zfft_process_device judges the whole call); crossovers measured by
  * tools/sweep_schedule.py (profiles/r04v/sweep_schedule.json).  Default tolerance: the
  * automatic zoom-8 choice (PC, paths 4/5, also for one frame per call) gives the float64
- * reference's decimated IQ within 5e-6 of its peak (measured 2-3e-6; path 1: 2e-6).
+ * reference's decimated IQ within 7e-6 of its peak (measured 2-5.3e-6; path 1: 2e-6).
  * 1 = blocked warm-up passes in the reference order (frames split over many waves),
  * 2 = blocked, fused commuted-order interior + exact edge windows, 3 = XA tiles (one wave per
  * frame and stage: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned;

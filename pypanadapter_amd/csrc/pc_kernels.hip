@@ -19,7 +19,9 @@
 
 // Diagnostic builds only (ZFFT_DIAG=1, never set by build.py): PC_KO timing knockouts with
 // wrong results by design -- 1 own-rate sections, 2 FIR gamma, 4 output-rate sections,
-// 8 K1's LO mix (and its table loads); KW only: 16 the two input-rate FIRs, 32 the input loads.
+// 8 K1's LO mix (and its table loads); KW only: 16 the two input-rate FIRs, 32 the input loads,
+// 64 the FIR sub-tile's barriers after the input and after FIR beta, 128 the two around the y1
+// hand-over (timing of the barriers alone: the LDS data races by design).
 #ifndef ZFFT_DIAG
 #define ZFFT_DIAG 0
 #endif
@@ -35,6 +37,19 @@ constexpr int kKo = 0;
 #endif
 #ifndef PC_STAMPS
 #define PC_STAMPS 0
+#endif
+// A/B knobs (diagnostic builds only): PC_DPPSHIFT = largest lane shift of the recurrence scans
+// done as a chain of whole-wave DPP shifts (wave_shr/shl:1) instead of one ds_bpermute
+// (default 1: only the first level); PC_PRIO = s_setprio level of the walk's recurrence phases
+// (own-rate and output-rate sections), the FIR phases running at 0 (default 0: no setprio).
+#if !ZFFT_DIAG && (defined(PC_DPPSHIFT) || defined(PC_PRIO))
+#error "PC_DPPSHIFT / PC_PRIO are diagnostic knobs: build with -DZFFT_DIAG"
+#endif
+#ifndef PC_DPPSHIFT
+#define PC_DPPSHIFT 1
+#endif
+#ifndef PC_PRIO
+#define PC_PRIO 0
 #endif
 
 namespace zfft {
@@ -78,6 +93,11 @@ __device__ __forceinline__ CT fresh(CT p) {
   return p;
 }
 __device__ __forceinline__ v2f lo2(v4f w) { return v2f{w.x, w.y}; }
+// lane k's v of a wave, for a wave-uniform k (v_readlane: an SGPR pair, no memory round trip)
+__device__ __forceinline__ v2f lane_val(v2f v, int k) {
+  return v2f{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), k)),
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), k))};
+}
 __device__ __forceinline__ v2f hi2(v4f w) { return v2f{w.z, w.w}; }
 __device__ __forceinline__ v4f cat(v2f a, v2f b) { return v4f{a.x, a.y, b.x, b.y}; }
 
@@ -164,8 +184,11 @@ __global__ void __launch_bounds__(256) pc_fir_kernel(InDesc in, const v2f *lo, v
   if (xs >= 0 && xs + kPcK1In <= L) {
     // LO factor lo[n0 + 2t + j] = lo[n0] lo[2t + j] / sqrt 2 (the table is an exact
     // exponential): one uniform entry per 512 samples instead of a table stream beside the
-    // input (which cost 13 % of the kernel, profiles/r04c)
+    // input (which cost 13 % of the kernel, profiles/r04c); the nine entries lo[xs + 512 k]
+    // are loaded by lanes k = 0..8 together with the input, and read back with v_readlane
+    // (issued one by one at their use, each load's round trip was exposed)
     const v4f lane_lo = *(const v4f *)(lor + 2 * t) * (float)M_SQRT1_2;
+    const v2f lo_k = lor[xs + 512 * min(t & 63, 8)];
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const int s = 2 * t + 512 * i;
@@ -175,7 +198,7 @@ __global__ void __launch_bounds__(256) pc_fir_kernel(InDesc in, const v2f *lo, v
       if constexpr (kKo & 8) {
         *(LP4)(xl + xidx(s)) = cat(a, b);
       } else {
-        const v2f c = lor[xs + 512 * i];  // uniform
+        const v2f c = lane_val(lo_k, i);  // lo[xs + 512 i]
         *(LP4)(xl + xidx(s)) = cat(cmul2(a, cmul2(c, lo2(lane_lo))), cmul2(b, cmul2(c, hi2(lane_lo))));
       }
     }
@@ -248,9 +271,21 @@ __device__ __forceinline__ v2f wshift(v2f v) {
 // instead of SH dependent DPP moves on the VALU.
 template <bool UP, int SH>
 __device__ __forceinline__ v2f shiftk(v2f v, int lane) {
-  const v2f r = UP ? v2f{__shfl_up(v.x, SH, 64), __shfl_up(v.y, SH, 64)}
-                   : v2f{__shfl_down(v.x, SH, 64), __shfl_down(v.y, SH, 64)};
-  return (UP ? lane < SH : lane >= 64 - SH) ? splat(0.f) : r;
+  if constexpr (SH <= PC_DPPSHIFT) {  // SH dependent DPP moves (diagnostic A/B form)
+#pragma unroll
+    for (int i = 0; i < SH; ++i) v = wshift<UP>(v);
+    return v;
+  } else {
+    const v2f r = UP ? v2f{__shfl_up(v.x, SH, 64), __shfl_up(v.y, SH, 64)}
+                     : v2f{__shfl_down(v.x, SH, 64), __shfl_down(v.y, SH, 64)};
+    return (UP ? lane < SH : lane >= 64 - SH) ? splat(0.f) : r;
+  }
+}
+__device__ __forceinline__ void walk_prio(bool recurrence) {
+  if constexpr (PC_PRIO > 0) {
+    if (recurrence) __builtin_amdgcn_s_setprio(PC_PRIO);
+    else __builtin_amdgcn_s_setprio(0);
+  }
 }
 
 // One all-pole section over this lane's block v[0..B) in time order (UP) or reversed (!UP),
@@ -522,13 +557,25 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
     }
   };
   prefetch(0);
+  // the LO table entries the fast sub-tiles of tile tau mix with, lo[xs_of(4 tau) + 512 k] for
+  // k = 8 c + i in [0, 32] (sub-tile c, chunk i): lane k holds entry k, loaded a tile ahead and
+  // read with v_readlane (a load per chunk at its use exposed the table's round trip in every
+  // sub-tile); clamped into the frame, which only the unused entries of edge tiles need
+  auto lo_chunks = [&](int tau_) -> v2f {
+    const int64_t n = xs_of(4 * tau_) + 512 * (int64_t)min(lane, 32);
+    return lor[n < 0 ? 0 : (n >= L ? L - 1 : n)];
+  };
+  v2f lo_nx = lo_chunks(0);
 #if PC_STAMPS
   unsigned long long st_acc[kPcStampSegs] = {}, t_prev;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_prev)::"memory");
 #endif
   for (int tau = 0; tau < ntiles; ++tau) {
     const int64_t m0 = kPcWM0 + (int64_t)kPcWM * tau;
+    const v2f lo_cur = lo_nx;
+    if (tau + 1 < ntiles) lo_nx = lo_chunks(tau + 1);
     // ---- FIRs: y2 for s in [1280, 5376), four sub-tiles
+    walk_prio(false);
     for (int c = 0; c < 4; ++c) {
       const int64_t xs = xs_of(4 * tau + c);  // first input sample (y2 from 2 m0 + 720 + 1024 c)
       if (fast(xs)) {
@@ -538,7 +585,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
           if (i == 8 && t >= (kPcK1In - 4096) / 2) break;
           v2f a, b;
           cvt_pair<DT, FLIP>(pf[i], a, b);
-          const v2f cc = lor[xs + 512 * i];  // uniform
+          const v2f cc = lane_val(lo_cur, 8 * c + i);  // lo[xs + 512 i]
           *(LP4)(xl + xidx(s)) = cat(cmul2(a, cmul2(cc, lo2(lane_lo))), cmul2(b, cmul2(cc, hi2(lane_lo))));
         }
         prefetch(4 * tau + c + 1);
@@ -551,7 +598,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
         }
         prefetch(4 * tau + c + 1);
       }
-      __syncthreads();
+      if constexpr (!(kKo & 64)) __syncthreads();
       PC_STAMP(0);
       v2f acc[8];
 #pragma unroll
@@ -571,14 +618,14 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
           }
         }
       }
-      __syncthreads();
+      if constexpr (!(kKo & 128)) __syncthreads();
       PC_STAMP(1);
       // y1 local i <-> 2 Q - 24 + i: [0, 48) carried, thread t's 8 at 48 + 8 t (row 6 + t)
       const LP yl = xl;
       if (t < 24) *(LP4)(yl + (t >> 2) * kYRow + 2 * (t & 3)) = y1c4[t];
 #pragma unroll
       for (int q = 0; q < 4; ++q) *(LP4)(yl + (6 + t) * kYRow + 2 * q) = cat(acc[2 * q], acc[2 * q + 1]);
-      __syncthreads();
+      if constexpr (!(kKo & 128)) __syncthreads();
       PC_STAMP(2);
       {
         v2f b[4];
@@ -602,10 +649,11 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
         *(LP4)(zo + 2) = cat(b[2], b[3]);
         if (t < 24) y1c4[t] = *(LP4)(yl + (256 + (t >> 2)) * kYRow + 2 * (t & 3));  // i = 2048 + 2 t
       }
-      __syncthreads();
+      if constexpr (!(kKo & 64)) __syncthreads();
       PC_STAMP(3);
     }
     // ---- own-rate sections, causal, on the new 4096 (carried states)
+    walk_prio(true);
     {
       v2f v[kPcWf];
       const LP zb = zl + zp(kPcWQ + kPcWf * t);  // a block of 16 never straddles a pad
@@ -654,6 +702,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
     __syncthreads();
     PC_STAMP(5);
     // ---- FIR gamma (K2's): u3 index k = 9 t + r (output m0 - 128 + k) from z s in [2k + 276, + 56]
+    walk_prio(false);
     {
       v2f u[9];
 #pragma unroll
@@ -679,6 +728,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
 #pragma unroll
     for (int r = 0; r < 4; ++r) zl[zp(4 * t) + r] = cz[r];
     // ---- output-rate sections (K2's: wave q takes outputs [512 q, + 512) with halos)
+    walk_prio(true);
     {
       v2f a[kPcApBlk];
       const int k0 = kU3Base - kPcApHalo + (kPcK2M / 4) * wave + kPcApBlk * lane;
