@@ -38,15 +38,17 @@ constexpr int kKo = 0;
 #ifndef PC_STAMPS
 #define PC_STAMPS 0
 #endif
-// A/B knobs (diagnostic builds only): PC_DPPSHIFT = largest lane shift of the recurrence scans
-// done as a chain of whole-wave DPP shifts (wave_shr/shl:1) instead of one ds_bpermute
-// (default 1: only the first level); PC_PRIO = s_setprio level of the walk's recurrence phases
-// (own-rate and output-rate sections), the FIR phases running at 0 (default 0: no setprio).
+// PC_DPPSHIFT = largest lane shift of the recurrence scans done as a chain of whole-wave DPP
+// shifts (wave_shr/shl:1, a few cycles each) instead of one ds_bpermute (an LDS round trip):
+// 4 -- shifts 1, 2, 4 by DPP, 8 and 16 by ds_bpermute (walk 1.5-3 % faster than 1 in three
+// same-box A/Bs, profiles/r05a, r05b, r05d; 16: no better).  A/B knobs (diagnostic builds only):
+// PC_DPPSHIFT, PC_PRIO = s_setprio level of the walk's recurrence phases (own-rate and
+// output-rate sections), the FIR phases running at 0 (default 0: no setprio; 2: within noise).
 #if !ZFFT_DIAG && (defined(PC_DPPSHIFT) || defined(PC_PRIO))
 #error "PC_DPPSHIFT / PC_PRIO are diagnostic knobs: build with -DZFFT_DIAG"
 #endif
 #ifndef PC_DPPSHIFT
-#define PC_DPPSHIFT 1
+#define PC_DPPSHIFT 4
 #endif
 #ifndef PC_PRIO
 #define PC_PRIO 0
