@@ -218,7 +218,9 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * rates + the slow poles as zero-phase sections at rates 1/4 and 1/8, two launches, plus
  * rank-~10 frame-end maps; frames >= 16384 samples, <= 65535 frames per launch), 5 = the
  * same arithmetic as one launch with one workgroup per frame (the rate-1/4 intermediate
- * stays on chip; automatic from 4096 frames per call).  Path 3
+ * stays on chip; automatic from 4096 frames per call); at zoom 4, path 5 is the two-stage
+ * form of the walk (FIR, own-rate sections at rate 1/2, 41-tap FIR, 6 output-rate sections;
+ * on request only: XA is faster there).  Path 3
  * needs every stage array below 2^31 bytes per frame; a forced path outside its domain
  * returns ZFFT_EUNSUPPORTED.  All produce the reference's rows within the fp32 parity gate
  * (zfft_plan.cpp auto_xa, use_fused, pc_fits). */

@@ -77,6 +77,7 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef v2f __attribute__((address_space(3))) *LP;
 typedef v4f __attribute__((address_space(3))) *LP4;
 typedef const PcTab __attribute__((address_space(4))) *CT;
+typedef const PcTab4 __attribute__((address_space(4))) *CT4;
 typedef const PcSec __attribute__((address_space(4))) &CS;
 
 __device__ __forceinline__ v2f shup(v2f v, int d) {
@@ -90,7 +91,8 @@ __device__ __forceinline__ v2f shxor(v2f v, int d) {
 }
 // An opaque copy of the table pointer per phase: the scalar loads of a phase's coefficients
 // are not hoisted out of it (hoisted, all 12 sections' tables would sit in SGPRs and spill).
-__device__ __forceinline__ CT fresh(CT p) {
+template <class P>
+__device__ __forceinline__ P fresh(P p) {
   asm volatile("" : "+s"(p));
   return p;
 }
@@ -357,6 +359,45 @@ __device__ __forceinline__ void ap_cascade(v2f (&a)[kPcApBlk], CT tab, int lane)
   sec_block<kPcApBlk, pc_ap_levels(S), pc_ap_dcut(S), UP, false, false, S>(a, tab, nullptr, lane, 0);
   if constexpr (S + 1 < kPcAp) ap_cascade<S + 1, UP>(a, tab, lane);
 }
+// zoom 4's output-rate cascade (PcTab4::ap, 6 sections): sec_block's arithmetic on its tables
+template <int B, int LEV, int DCUT, bool UP>
+__device__ __forceinline__ void sec_run(v2f (&v)[B], CS S, int lane) {
+  const v2f na1 = splat(-S.a1), na2 = splat(-S.a2);
+  v2f y1 = splat(0.f), y2 = splat(0.f);
+#pragma unroll
+  for (int c = 0; c < B; ++c) {
+    const int k = UP ? c : B - 1 - c;
+    const v2f y = vfma(na1, y1, vfma(na2, y2, v[k]));
+    y2 = y1;
+    y1 = y;
+    v[k] = y;
+  }
+  v2f e0 = y1, e1 = y2;
+#pragma unroll
+  for (int d = 0; d < LEV; ++d) {
+    v2f p0, p1;
+    if (d == 0) p0 = wshift<UP>(e0), p1 = wshift<UP>(e1);
+    else if (d == 1) p0 = shiftk<UP, 2>(e0, lane), p1 = shiftk<UP, 2>(e1, lane);
+    else if (d == 2) p0 = shiftk<UP, 4>(e0, lane), p1 = shiftk<UP, 4>(e1, lane);
+    else p0 = shiftk<UP, 8>(e0, lane), p1 = shiftk<UP, 8>(e1, lane);
+    const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
+    e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
+    e0 = n0;
+  }
+  v2f i0 = wshift<UP>(e0), i1 = wshift<UP>(e1);
+  if (lane == (UP ? 0 : 63)) i0 = i1 = splat(0.f);
+#pragma unroll
+  for (int c = 0; c < DCUT; ++c) {
+    const int k = UP ? c : B - 1 - c;
+    v[k] = vfma(splat(S.ct[c][0]), i0, vfma(splat(S.ct[c][1]), i1, v[k]));
+  }
+}
+template <int S, bool UP>
+__device__ __forceinline__ void ap_cascade(v2f (&a)[kPcApBlk], CT4 tab0, int lane) {
+  const CT4 tab = fresh(tab0);
+  sec_run<kPcApBlk, pc4_ap_levels(S), pc4_ap_dcut(S), UP>(a, tab->ap[S], lane);
+  if constexpr (S + 1 < kPc4Ap) ap_cascade<S + 1, UP>(a, tab, lane);
+}
 
 constexpr int kU3 = 256 * 9;                   // FIR gamma outputs per tile (9 per thread)
 constexpr int kU3Base = 128;                    // u3 index k <-> output m0 - 128 + k
@@ -454,9 +495,9 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
 // sec_block for KW: own-rate section SI (causal: table wf, B = 16; anticausal: wb, B = 20)
 // over the 4 waves' lane blocks, the waves continuing each other; the first wave in time
 // order enters with (c0, c1): the state carried from the previous tile (causal) or 0.
-template <int B, int LEV, bool UP, int SI>
-__device__ __forceinline__ void wsec(v2f (&v)[B], CT tab0, LP scr, int lane, int wave, v2f c0, v2f c1) {
-  const CT tab = fresh(tab0);
+template <int B, int LEV, bool UP, int SI, class TP>
+__device__ __forceinline__ void wsec(v2f (&v)[B], TP tab0, LP scr, int lane, int wave, v2f c0, v2f c1) {
+  const TP tab = fresh(tab0);
   CS S = UP ? tab->wf[SI] : tab->wb[SI];
   const v2f na1 = splat(-S.a1), na2 = splat(-S.a2);
   v2f y1 = splat(0.f), y2 = splat(0.f);
@@ -529,8 +570,27 @@ static_assert(kOutOff + kPcK2M <= kXRows * kXRow, "KW: u3 + outputs fit the inpu
 // state carried from the previous tile; the anticausal ones on s in [256, 5376) from a zero
 // state at the top (s >= 4938 is warm-up only: 0.935^438 < 1e-12), whose lower 1024 are the
 // previous tile's top causal outputs; then K2's FIR gamma and output-rate sections.
-template <int DT, int FLIP>
-__global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, CT tab) {
+// ZOOM = 4 (PcTab4): the same walk one stage shorter -- per tile two sub-tiles of 2048 y1 (the
+// same 4128-sample input tile and FIR alpha) written straight into the own-rate span (y1 is
+// zoom 4's own-rate signal), then the own-rate sections, FIR g1 (41 taps, gamma's place) and
+// 6 output-rate sections.
+template <int ZOOM> struct WalkZ;
+template <> struct WalkZ<8> {
+  typedef CT Tab;
+  static constexpr int SUB = 4, WM0 = kPcWM0, G = kPcG2;
+  // sub-tile g's first input sample (y2 from 2 m0 + 720 + 1024 c, the y1 carry of 48 below it)
+  static __device__ __forceinline__ int64_t xs_of(int g) { return 4 * (2 * (int64_t)WM0 + 720 + (int64_t)kPcWQ * g) + 32; }
+};
+template <> struct WalkZ<4> {
+  typedef CT4 Tab;
+  static constexpr int SUB = 2, WM0 = kPc4WM0, G = kPc4G1;
+  // y1 local i <-> m = xs / 2 + 8 + i; sub-tile g makes y1 from 2 m0 + 720 + 2048 c
+  static __device__ __forceinline__ int64_t xs_of(int g) { return 2 * (2 * (int64_t)WM0 + 720 + 2048 * (int64_t)g) - 16; }
+};
+template <int DT, int FLIP, int ZOOM>
+__global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3,
+                                                      typename WalkZ<ZOOM>::Tab tab) {
+  using Z = WalkZ<ZOOM>;
   __shared__ v4f xl4[kXRows * kXRow / 2];  // K1 input tile, then y1; then u3 + staged outputs
   __shared__ v4f z4[kWZP / 2];             // own-rate samples, span s in [256, 5376)
   __shared__ v4f scr4[16];                 // cross-wave states (4 section calls)
@@ -544,15 +604,15 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
   for (int i = t; i < kPcWQ; i += 256) zl[zp(i)] = splat(0.f);
   if (t < 24) y1c4[t] = v4f{0.f, 0.f, 0.f, 0.f};
   if (t < 2) car4[t] = v4f{0.f, 0.f, 0.f, 0.f};
-  const int ntiles = (int)((n3 - kPcWM0 + kPcWM - 1) / kPcWM);
+  const int ntiles = (int)((n3 - Z::WM0 + kPcWM - 1) / kPcWM);
   // sub-tile g's first input sample; inside the frame ("fast") its pairs are prefetched into
   // registers one sub-tile ahead (the first of a tile during the previous tile's sections)
-  auto xs_of = [&](int g) { return 4 * (2 * (int64_t)kPcWM0 + 720 + (int64_t)kPcWQ * g) + 32; };
+  auto xs_of = [&](int g) { return Z::xs_of(g); };
   auto fast = [&](int64_t xs) { return xs >= 0 && xs + kPcK1In <= L; };
   typename RawP<DT>::T pf[9];
   auto prefetch = [&](int g) {
     const int64_t xs = xs_of(g);
-    if (g < 4 * ntiles && fast(xs) && !(kKo & 32)) {
+    if (g < Z::SUB * ntiles && fast(xs) && !(kKo & 32)) {
 #pragma unroll
       for (int i = 0; i < 9; ++i)
         if (i < 8 || t < (kPcK1In - 4096) / 2) pf[i] = raw_pair<DT, FLIP>(in, f, xs + 2 * t + 512 * i);
@@ -564,7 +624,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
   // read with v_readlane (a load per chunk at its use exposed the table's round trip in every
   // sub-tile); clamped into the frame, which only the unused entries of edge tiles need
   auto lo_chunks = [&](int tau_) -> v2f {
-    const int64_t n = xs_of(4 * tau_) + 512 * (int64_t)min(lane, 32);
+    const int64_t n = xs_of(Z::SUB * tau_) + 512 * (int64_t)min(lane, 8 * Z::SUB);
     return lor[n < 0 ? 0 : (n >= L ? L - 1 : n)];
   };
   v2f lo_nx = lo_chunks(0);
@@ -573,13 +633,13 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_prev)::"memory");
 #endif
   for (int tau = 0; tau < ntiles; ++tau) {
-    const int64_t m0 = kPcWM0 + (int64_t)kPcWM * tau;
+    const int64_t m0 = Z::WM0 + (int64_t)kPcWM * tau;
     const v2f lo_cur = lo_nx;
     if (tau + 1 < ntiles) lo_nx = lo_chunks(tau + 1);
     // ---- FIRs: y2 for s in [1280, 5376), four sub-tiles
     walk_prio(false);
-    for (int c = 0; c < 4; ++c) {
-      const int64_t xs = xs_of(4 * tau + c);  // first input sample (y2 from 2 m0 + 720 + 1024 c)
+    for (int c = 0; c < Z::SUB; ++c) {
+      const int64_t xs = xs_of(Z::SUB * tau + c);  // first input sample
       if (fast(xs)) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
@@ -590,7 +650,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
           const v2f cc = lane_val(lo_cur, 8 * c + i);  // lo[xs + 512 i]
           *(LP4)(xl + xidx(s)) = cat(cmul2(a, cmul2(cc, lo2(lane_lo))), cmul2(b, cmul2(cc, hi2(lane_lo))));
         }
-        prefetch(4 * tau + c + 1);
+        prefetch(Z::SUB * tau + c + 1);
       } else {
         for (int s = t; s < kPcK1In; s += 256) {
           const int64_t n = xs + s;
@@ -598,7 +658,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
           if (n >= 0 && n < L) v = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
           xl[xidx(s)] = v;
         }
-        prefetch(4 * tau + c + 1);
+        prefetch(Z::SUB * tau + c + 1);
       }
       if constexpr (!(kKo & 64)) __syncthreads();
       PC_STAMP(0);
@@ -622,6 +682,12 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
       }
       if constexpr (!(kKo & 128)) __syncthreads();
       PC_STAMP(1);
+      if constexpr (ZOOM == 4) {  // y1 local 8 t + r -> span index 1280 + 2048 c + 8 t + r
+        const LP zo = zl + zp(kPcWQ + 2048 * c + 8 * t);  // 8 never straddle a pad
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *(LP4)(zo + 2 * q) = cat(acc[2 * q], acc[2 * q + 1]);
+        continue;  // the next sub-tile's input overwrites xl: every alpha read is done
+      } else {
       // y1 local i <-> 2 Q - 24 + i: [0, 48) carried, thread t's 8 at 48 + 8 t (row 6 + t)
       const LP yl = xl;
       if (t < 24) *(LP4)(yl + (t >> 2) * kYRow + 2 * (t & 3)) = y1c4[t];
@@ -653,7 +719,9 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
       }
       if constexpr (!(kKo & 64)) __syncthreads();
       PC_STAMP(3);
+      }
     }
+    if constexpr (ZOOM == 4) __syncthreads();  // the span's new y1 are in
     // ---- own-rate sections, causal, on the new 4096 (carried states)
     walk_prio(true);
     {
@@ -709,17 +777,23 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
       v2f u[9];
 #pragma unroll
       for (int r = 0; r < 9; ++r) u[r] = splat(0.f);
-      const LP zb = zl + 18 * t + (kPcK2Left - 2 * kU3Base) - (kPcG2 - 1) / 2 - 256;
+      // zoom 8: g2 (57 taps) on z2 at rate 1/4; zoom 4: g1 (41 taps) on z1 at rate 1/2
+      constexpr int G = Z::G;
+      const auto taps = [&]() {
+        if constexpr (ZOOM == 8) return tab->g2;
+        else return tab->g1;
+      };
+      const LP zb = zl + 18 * t + (kPcK2Left - 2 * kU3Base) - (G - 1) / 2 - 256;
 #pragma unroll
-      for (int p = 0; p < ((kKo & 2) ? 1 : 37); ++p) {
+      for (int p = 0; p < ((kKo & 2) ? 1 : (G + 17) / 2); ++p) {
         const int j = 2 * p;
         const v4f w = *(LP4)(zb + j);
         const v2f x0 = lo2(w), x1 = hi2(w);
 #pragma unroll
         for (int r = 0; r < 9; ++r) {
           const int q = j - 2 * r;
-          if (q >= 0 && q < kPcG2) u[r] = vfma(splat(tab->g2[q]), x0, u[r]);
-          if (q + 1 >= 0 && q + 1 < kPcG2) u[r] = vfma(splat(tab->g2[q + 1]), x1, u[r]);
+          if (q >= 0 && q < G) u[r] = vfma(splat(taps()[q]), x0, u[r]);
+          if (q + 1 >= 0 && q + 1 < G) u[r] = vfma(splat(taps()[q + 1]), x1, u[r]);
         }
       }
 #pragma unroll
@@ -841,6 +915,22 @@ extern "C" int zfft_debug_pc_stamps(unsigned long long *out) {
     }                                                                                            \
   } while (0)
 
+#define PC_LAUNCH2Z(KERNEL, DT, fl, Z, ...)                                                     \
+  do {                                                                                           \
+    if (fl) hipLaunchKernelGGL((KERNEL<DT, 1, Z>), __VA_ARGS__);                                 \
+    else hipLaunchKernelGGL((KERNEL<DT, 0, Z>), __VA_ARGS__);                                    \
+  } while (0)
+#define PC_DISPATCH_Z(KERNEL, Z, in, ...)                                                        \
+  do {                                                                                           \
+    const bool fl = (in).flip != 0;                                                              \
+    switch ((in).dtype) {                                                                        \
+      case kInC64: PC_LAUNCH2Z(KERNEL, kInC64, fl, Z, __VA_ARGS__); break;                       \
+      case kInC32H: PC_LAUNCH2Z(KERNEL, kInC32H, fl, Z, __VA_ARGS__); break;                     \
+      case kInCU8: PC_LAUNCH2Z(KERNEL, kInCU8, fl, Z, __VA_ARGS__); break;                       \
+      default: PC_LAUNCH2Z(KERNEL, kInF32R, fl, Z, __VA_ARGS__); break;                          \
+    }                                                                                            \
+  } while (0)
+
 hipError_t launch_pc_fir(const InDesc &in, const float2 *lo, float2 *y2, int64_t y2_stride,
                          int frames, const PcTab *tab, hipStream_t st) {
   const int ntiles = (int)((pc_y2_len(in.len) + kPcK1Q - 1) / kPcK1Q);
@@ -861,8 +951,15 @@ hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int6
 
 hipError_t launch_pc_walk(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
                           const PcTab *tab, hipStream_t st) {
-  PC_DISPATCH(pc::pc_walk_kernel, in, dim3((unsigned)frames), dim3(256), 0, st, in, (const v2f *)lo,
-              (v2f *)out, n3, (pc::CT)tab);
+  PC_DISPATCH_Z(pc::pc_walk_kernel, 8, in, dim3((unsigned)frames), dim3(256), 0, st, in, (const v2f *)lo,
+                (v2f *)out, n3, (pc::CT)tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_pc_walk4(const InDesc &in, const float2 *lo, float2 *out, int64_t n2, int frames,
+                           const PcTab4 *tab, hipStream_t st) {
+  PC_DISPATCH_Z(pc::pc_walk_kernel, 4, in, dim3((unsigned)frames), dim3(256), 0, st, in, (const v2f *)lo,
+                (v2f *)out, n2, (pc::CT4)tab);
   return hipGetLastError();
 }
 

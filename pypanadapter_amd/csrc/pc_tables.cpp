@@ -175,8 +175,8 @@ void exact_stage(const std::vector<double> &x, std::vector<double> &out) {
   for (int j = 0; j < (int)out.size(); ++j) out[j] = ext[P + 2 * j];
 }
 
-void exact3(std::vector<double> x, std::vector<double> &out) {
-  for (int k = 0; k < kPcStages; ++k) {
+void exact_k(std::vector<double> x, int K, std::vector<double> &out) {  // decimate(., 2)^K
+  for (int k = 0; k < K; ++k) {
     exact_stage(x, out);
     x.swap(out);
   }
@@ -203,16 +203,16 @@ void fft_inplace(std::vector<std::complex<double>> &a, bool inverse) {
   }
 }
 
-// Impulse response of the LTI model G(z) = prod_k |H(z^(2^k))|^2 at the input rate,
-// h[n] for |n| < kHz (the model output m is sum_n h[8m - n] x[n]).
+// Impulse response of the LTI model G(z) = prod_(k < K) |H(z^(2^k))|^2 at the input rate,
+// h[n] for |n| < kHz (the model output m is sum_n h[2^K m - n] x[n]).
 constexpr int kHzFft = 1 << 16, kHz = 1 << 15;
-const std::vector<double> &model_hz() {
-  static const std::vector<double> H = [] {
+std::vector<double> model_hz_build(int K) {
+  {
     std::vector<std::complex<double>> g(kHzFft);
     for (int k = 0; k < kHzFft; ++k) {
       const double w = 2.0 * M_PI * k / kHzFft;
       double G = 1.0;
-      for (int s = 0; s < kPcStages; ++s) {
+      for (int s = 0; s < K; ++s) {
         const double ws = w * (double)(1 << s);
         std::complex<double> h(1.0, 0.0);
         const std::complex<double> e1 = std::polar(1.0, -ws), e2 = std::polar(1.0, -2 * ws);
@@ -228,17 +228,20 @@ const std::vector<double> &model_hz() {
     std::vector<double> h(2 * kHz + 1);
     for (int n = -kHz; n <= kHz; ++n) h[n + kHz] = g[(n + kHzFft) % kHzFft].real() / kHzFft;
     return h;
-  }();
-  return H;
+  }
+}
+const std::vector<double> &model_hz(int K) {
+  static const std::vector<double> H2 = model_hz_build(2), H3 = model_hz_build(3);
+  return K == 2 ? H2 : H3;
 }
 
-// C[m][j] = (exact - model)(e_j) at output m; side 0 from the frame start, side 1 from the
-// frame end (frame length = lmod8 mod 8).
-void edge_matrix(int side, int lmod8, int R, int J, std::vector<double> &C) {
-  const int Lc = 4096 + lmod8;
+// C[m][j] = (exact - model)(e_j) at output m of K stages; side 0 from the frame start, side 1
+// from the frame end (frame length = lmod mod 2^K).
+void edge_matrix(int K, int side, int lmod, int R, int J, std::vector<double> &C) {
+  const int Lc = 4096 + lmod;
   int n3 = Lc;
-  for (int k = 0; k < kPcStages; ++k) n3 = (n3 + 1) / 2;
-  const std::vector<double> &hz = model_hz();
+  for (int k = 0; k < K; ++k) n3 = (n3 + 1) / 2;
+  const std::vector<double> &hz = model_hz(K);
   C.assign((size_t)R * J, 0.0);
   const int nt = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
   auto work = [&](int w) {
@@ -247,10 +250,10 @@ void edge_matrix(int side, int lmod8, int R, int J, std::vector<double> &C) {
       const int pos = side == 0 ? j : Lc - 1 - j;
       std::fill(x.begin(), x.end(), 0.0);
       x[pos] = 1.0;
-      exact3(x, out);
+      exact_k(x, K, out);
       for (int m = 0; m < R; ++m) {
         const int mo = side == 0 ? m : n3 - 1 - m;
-        const long n = 8L * mo - pos;
+        const long n = (1L << K) * mo - pos;
         const double model = (n >= -kHz && n <= kHz) ? hz[n + kHz] : 0.0;
         C[(size_t)m * J + j] = out[mo] - model;
       }
@@ -320,10 +323,38 @@ bool pc_build_tables(PcTab &tab) {
   return true;
 }
 
-bool pc_edge_map(int side, int lmod8, PcEdge &out) {
+bool pc_build_tables4(PcTab4 &tab) {
+  std::memset(&tab, 0, sizeof(tab));
+  const Lev &l = levels();
+  const Poly f0 = conv(l.n9, neg(sec_poly(l.d[0], {0, 1, 2, 3})));
+  const Poly f1 = conv(conv(l.n9, neg(sec_poly(l.d[1], {0, 1, 2, 3}))), neg(sec_poly(l.d[0], {0, 1})));
+  const Poly g0 = zero_phase(f0), g1 = zero_phase(f1);
+  if ((int)g0.size() != kPcG0 || (int)g1.size() != kPc4G1) return false;
+  for (int i = 0; i < kPcG0; ++i) tab.g0[i] = (float)g0[i];
+  for (int i = 0; i < kPc4G1; ++i) tab.g1[i] = (float)g1[i];
+  PcTab t8;  // the own-rate sections are zoom 8's (the base filter's sections 2, 3)
+  if (!pc_build_tables(t8)) return false;
+  std::memcpy(tab.wf, t8.wf, sizeof(tab.wf));
+  std::memcpy(tab.wb, t8.wb, sizeof(tab.wb));
+  std::memcpy(tab.wf_x, t8.wf_x, sizeof(tab.wf_x));
+  std::memcpy(tab.wb_x, t8.wb_x, sizeof(tab.wb_x));
+  // output-rate sections: D4 (stage 0 moved twice), D2 sections 0, 1 (stage 1), slowest first
+  std::vector<std::pair<double, double>> ap;
+  for (int k = 0; k < 4; ++k) ap.emplace_back(l.d[2].a1[k], l.d[2].a2[k]);
+  for (int k = 0; k < 2; ++k) ap.emplace_back(l.d[1].a1[k], l.d[1].a2[k]);
+  std::stable_sort(ap.begin(), ap.end(), [](auto &a, auto &b) { return a.second > b.second; });
+  for (int s = 0; s < kPc4Ap; ++s)
+    if (!sec_tables(ap[s].first, ap[s].second, kPcApBlk, pc4_ap_levels(s), pc4_ap_dcut(s), tab.ap[s]))
+      return false;
+  return true;
+}
+
+bool pc_edge_map(int side, int lmod8, PcEdge &out) { return pc_edge_map_k(3, side, lmod8, out); }
+
+bool pc_edge_map_k(int K, int side, int lmod, PcEdge &out) {
   const int R = kPcEdgeR, J = side == 0 ? 768 : kPcEdgeJ;
   std::vector<double> C;
-  edge_matrix(side, lmod8, R, J, C);
+  edge_matrix(K, side, lmod & ((1 << K) - 1), R, J, C);
   // entries are responses to unit input samples: below kTol they cannot move an output by
   // more than ~1e-9 of the input's peak even summed over a whole edge
   constexpr double kTol = 1e-11;
@@ -401,7 +432,9 @@ bool pc_edge_map(int side, int lmod8, PcEdge &out) {
 // Test hook (not part of include/zfft.h): the PC tables, for the CPU suite.
 //   what 0: FIR taps g0 | g1 | g2 (139 floats); 1: PcTab as raw floats;
 //   2 / 3: left / right edge map for L mod 8 = arg built now (fp64): R, J, r then U (R x r), V (J x r);
-//   4: the shipped constant map arg of pc_edge_maps.h: R, J, r then U (R x r), V^T (r x J).
+//   4: the shipped constant map arg of pc_edge_maps.h: R, J, r then U (R x r), V^T (r x J);
+//   5: zoom 4 FIR taps g0 | g1 (74 floats); 12 / 13: zoom-4 left / right map for L mod 4 = arg
+//   built now; 14: the shipped zoom-4 map arg.
 extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
   using namespace zfft;
   if (what == 0 || what == 1) {
@@ -420,9 +453,34 @@ extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
     std::memcpy(out, &t, sizeof(t));
     return n;
   }
-  if (what == 4) {  // the shipped constant map arg (0 start, 1 + k end for L mod 8 = k)
-    if (arg < 0 || arg >= kPcEdgeMaps) return -3;
-    const PcEdgeConst &m = kPcEdgeIdx[arg];
+  if (what == 5) {  // zoom 4: FIR taps g0 | g1 (33 + 41 floats)
+    PcTab4 t;
+    if (!pc_build_tables4(t)) return -1;
+    if (cap < kPcG0 + kPc4G1) return -2;
+    std::memcpy(out, t.g0, kPcG0 * 4);
+    std::memcpy(out + kPcG0, t.g1, kPc4G1 * 4);
+    return kPcG0 + kPc4G1;
+  }
+  if (what == 12 || what == 13) {  // zoom 4: left / right map for L mod 4 = arg, built now
+    PcEdge e;
+    try {
+      if (!pc_edge_map_k(2, what - 12, arg & 3, e)) return -1;
+    } catch (...) {
+      return -4;
+    }
+    const int n = 3 + e.R * e.r + e.J * e.r;
+    if (cap < n) return -2;
+    out[0] = (float)e.R;
+    out[1] = (float)e.J;
+    out[2] = (float)e.r;
+    std::copy(e.U.begin(), e.U.end(), out + 3);
+    std::copy(e.V.begin(), e.V.end(), out + 3 + e.R * e.r);
+    return n;
+  }
+  if (what == 4 || what == 14) {  // the shipped constant map arg (0 start, 1 + k end for L mod
+                                  // 2^K = k): zoom 8 (4), zoom 4 (14)
+    if (arg < 0 || arg >= (what == 4 ? kPcEdgeMaps : kPcEdge4Maps)) return -3;
+    const PcEdgeConst &m = what == 4 ? kPcEdgeIdx[arg] : kPcEdge4Idx[arg];
     const int n = 3 + m.R * m.r + m.J * m.r;
     if (cap < n) return -2;
     out[0] = (float)m.R;

@@ -185,6 +185,24 @@ __host__ __device__ constexpr int pc_ap_levels(int s) {
   return s == 0 ? 3 : s <= 3 ? 2 : s <= 6 ? 1 : 0;
 }
 __host__ __device__ constexpr int pc_ap_dcut(int s) { return s < 8 ? kPcApBlk : s == 8 ? 8 : 6; }
+// Zoom 4 (two stages): the same construction one stage shorter --
+//   y1 = (g0 * x)|2                 FIR (33 taps; stage 0's poles moved to the output rate)
+//   z1 = S(u) S(1/u) y1             stage 1's two slowest sections at their own rate (= wf, wb)
+//   u2 = (g1 * z1)|2                FIR (41 taps: N D2(-u) D{0,1}(-u), zero phase)
+//   out = A(w) A(1/w) u2            6 sections at the output rate (D4, D2{0,1}; radius <= .765)
+// run by the walk only (pc_walk_kernel<ZOOM = 4>): per tile two FIR sub-tiles of 2048 y1 (the
+// input tile of zoom 8's sub-tile) go straight into the own-rate span.
+constexpr int kPc4G1 = 41, kPc4Ap = 6;
+constexpr int kPc4WM0 = -364;            // first tile's m0: its FIR tile starts at y1 index -8
+struct PcTab4 {
+  float g0[36], g1[44];             // zero-phase FIR taps (centred)
+  PcSec ap[kPc4Ap];                 // B = 11, slowest first
+  PcSec wf[kPcOwn], wb[kPcOwn];     // own-rate sections (those of PcTab)
+  float wf_x[kPcOwn][64][4], wb_x[kPcOwn][64][4];
+};
+__host__ __device__ constexpr int pc4_ap_levels(int s) { return s == 0 ? 3 : s <= 2 ? 2 : s <= 4 ? 1 : 0; }
+__host__ __device__ constexpr int pc4_ap_dcut(int) { return kPcApBlk; }
+bool pc_build_tables4(PcTab4 &tab);
 // Frame-end maps, out[m] += sum_k U[m][k] (sum_j V[j][k] x[j]) (left: m, j from the start;
 // right: from the end), rank r.
 struct PcEdge {
@@ -192,8 +210,9 @@ struct PcEdge {
   std::vector<float> U, V;         // R x r, J x r (row-major)
 };
 bool pc_build_tables(PcTab &tab);
-// side 0 = frame start, 1 = frame end (depends on L mod 8)
+// side 0 = frame start, 1 = frame end (depends on L mod 8); _k: K stages (zoom 2^K, L mod 2^K)
 bool pc_edge_map(int side, int lmod8, PcEdge &out);
+bool pc_edge_map_k(int K, int side, int lmod, PcEdge &out);
 int64_t pc_y2_len(int64_t L);      // y2 entries per frame (from kPcQ0)
 hipError_t launch_pc_fir(const InDesc &in, const float2 *lo, float2 *y2, int64_t y2_stride,
                          int frames, const PcTab *tab, hipStream_t st);
@@ -201,6 +220,8 @@ hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int6
                           int frames, const PcTab *tab, hipStream_t st);
 hipError_t launch_pc_walk(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
                           const PcTab *tab, hipStream_t st);
+hipError_t launch_pc_walk4(const InDesc &in, const float2 *lo, float2 *out, int64_t n2, int frames,
+                           const PcTab4 *tab, hipStream_t st);
 // both frame ends in one launch: [0] = start, [1] = end
 hipError_t launch_pc_edge(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
                           const float *const U[2], const float *const V[2], const int R[2],

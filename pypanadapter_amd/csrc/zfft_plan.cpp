@@ -405,6 +405,7 @@ struct zfft_plan {
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
   DevBuf edge, xk, xa_tab, tws, means, z4, winf;
   DevBuf pc_tab, pc_edge;  // PC decimator: PcTab; edge maps U0 V0 U1 V1 (floats)
+  DevBuf pc_tab4;          // PC zoom 4: PcTab4
                            // (pc_edge: all nine maps of pc_edge_maps.h, uploaded once)
   int64_t n_quiesce = 0;   // host waits on enqueued work (test hook zfft__plan_quiesce_count)
   // waterfall rendering: colormap LUT (host copy + device), levels
@@ -788,6 +789,13 @@ constexpr int kPcWalkMinFrames = 4096;
 bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == kPcStages && L >= kPcMinL && frames <= 65535;
 }
+// Zoom 4 (two stages) has the walk form only (pc_walk_kernel<4>), on request (path 5): at cfg1
+// (F = 4096, L = 262,144) it takes 4.49-4.50 ms against XA's 2.89 + 1.45 = 4.34 ms on the same
+// box (profiles/r05h) -- at zoom 4 the recurrences run on twice the share of the samples they
+// see at zoom 8, and they are the walk's latency-bound half -- so the automatic choice stays XA.
+bool pc4_fits(const zfft_plan *p, int64_t L, int frames) {
+  return p->K == 2 && L >= kPcMinL && frames <= 65535;
+}
 
 // Host copy of the PC tables: built once per process (fp64, microseconds); the frame-end maps
 // are the constants of pc_edge_maps.h (tools/gen_pc_edge.py).
@@ -799,17 +807,31 @@ const PcTab *pc_host_tab() {
   }();
   return t.get();
 }
+const PcTab4 *pc_host_tab4() {
+  static const std::unique_ptr<PcTab4> t = [] {
+    std::unique_ptr<PcTab4> x(new PcTab4());
+    if (!pc_build_tables4(*x)) x.reset();
+    return x;
+  }();
+  return t.get();
+}
 // The PC tables and all nine frame-end maps, uploaded on the plan's first PC call; nothing is
 // uploaded afterwards, so a change of L mod 8 between calls never waits on enqueued work.
 int ensure_pc(zfft_plan *p) {
-  if (p->pc_tab.p && p->pc_edge.p) return ZFFT_OK;
+  if (p->pc_tab.p && p->pc_tab4.p && p->pc_edge.p) return ZFFT_OK;
   const PcTab *t = pc_host_tab();
-  if (!t) return fail(ZFFT_EINTERNAL, "PC tables: scan depth or correction length too short");
+  const PcTab4 *t4 = pc_host_tab4();
+  if (!t || !t4) return fail(ZFFT_EINTERNAL, "PC tables: scan depth or correction length too short");
   for (const PcEdgeConst &m : kPcEdgeIdx)
+    if (m.r > kPcEdgeRank || m.R > kPcEdgeR || m.R > 256)
+      return fail(ZFFT_EINTERNAL, "PC frame-end maps exceed the kernel's capacities");
+  for (const PcEdgeConst &m : kPcEdge4Idx)
     if (m.r > kPcEdgeRank || m.R > kPcEdgeR || m.R > 256)
       return fail(ZFFT_EINTERNAL, "PC frame-end maps exceed the kernel's capacities");
   hipError_t e = p->pc_tab.ensure(sizeof(PcTab));
   if (e == hipSuccess) e = hipMemcpy(p->pc_tab.p, t, sizeof(PcTab), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = p->pc_tab4.ensure(sizeof(PcTab4));
+  if (e == hipSuccess) e = hipMemcpy(p->pc_tab4.p, t4, sizeof(PcTab4), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = p->pc_edge.ensure(sizeof(kPcEdgeData));
   if (e == hipSuccess) e = hipMemcpy(p->pc_edge.p, kPcEdgeData, sizeof(kPcEdgeData), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "PC table upload");
@@ -825,7 +847,13 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
   const int64_t n3 = n[p->K];
   const PcTab *tab = p->pc_tab.as<PcTab>();
   hipError_t e;
-  if (walk) {  // one launch, y2 in LDS
+  if (p->K == 2) {  // zoom 4: the walk only
+    e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+    e = launch_pc_walk4(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab4.as<PcTab4>(), st);
+    if (e != hipSuccess) return hip_fail(e, "pc_walk4 launch");
+    mark(p, st, "pc_walk4");
+  } else if (walk) {  // one launch, y2 in LDS
     e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
     e = launch_pc_walk(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, tab, st);
@@ -843,9 +871,10 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
     if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
     mark(p, st, "pc_tail");
   }
-  // map 0 = frame start, 1 + (L mod 8) = frame end (pc_edge_maps.h)
+  // map 0 = frame start, 1 + (L mod 2^K) = frame end (pc_edge_maps.h)
   const float *eb = p->pc_edge.as<float>();
-  const PcEdgeConst &m0 = kPcEdgeIdx[0], &m1 = kPcEdgeIdx[1 + (L & 7)];
+  const PcEdgeConst &m0 = p->K == 2 ? kPcEdge4Idx[0] : kPcEdgeIdx[0];
+  const PcEdgeConst &m1 = p->K == 2 ? kPcEdge4Idx[1 + (L & 3)] : kPcEdgeIdx[1 + (L & 7)];
   const float *const U[2] = {eb + m0.u, eb + m1.u};
   const float *const V[2] = {eb + m0.v, eb + m1.v};
   const int R[2] = {m0.R, m1.R}, J[2] = {m0.J, m1.J}, r[2] = {m0.r, m1.r};
@@ -865,9 +894,10 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  if ((p->path == 4 || p->path == 5) && !pc_fits(p, L, frames))
-    return fail(ZFFT_EUNSUPPORTED, "PC decimator (paths 4, 5) needs zoom 8, frames of >= 16384 "
-                                   "samples and <= 65535 frames per call");
+  if ((p->path == 4 && !pc_fits(p, L, frames)) || (p->path == 5 && !pc_fits(p, L, frames) && !pc4_fits(p, L, frames)))
+    return fail(ZFFT_EUNSUPPORTED, "PC decimator needs zoom 8 (path 4, 5) or zoom 4 (path 5), frames "
+                                   "of >= 16384 samples and <= 65535 frames per call");
+  if (p->path == 5 && pc4_fits(p, L, frames)) return run_pc(p, in, L, frames, n, true, out, st);
   // PC is the fastest schedule wherever it applies, from one frame per call (the
   // reference's use: 0.083 against 0.37 ms for path 1) to full batches (1024 frames: 1.44
   // against 2.03 ms for XA) -- tools/sweep_schedule.py, profiles/r04l

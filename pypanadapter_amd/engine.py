@@ -120,7 +120,8 @@ class ZoomFFT:
         samples per call), 3 XA tiles (all-pole + FIR + half-rate all-pole, one wave per
         frame; auto for >= 768 frames, or >= 384 frames of <= 2^19 samples), 4 PC polyphase
         cascade tiles (zoom 8, frames >= 16384 samples; the auto choice there below 4096
-        frames per call), 5 the PC walk (one workgroup per frame; auto from 4096 frames)."""
+        frames per call), 5 the PC walk (one workgroup per frame; zoom 8: auto from 4096
+        frames; zoom 4: the two-stage walk, on request only -- XA is faster there)."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")
 
     def set_welch(self, mode: int) -> None:

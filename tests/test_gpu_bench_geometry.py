@@ -25,7 +25,7 @@ def torch_dev():
 
 @pytest.mark.parametrize("config,in_dtype", [("cfg2", "complex64"), ("cfg3", "complex64"),
                                              ("cfg5", "complex64"), ("cfg2", "cu8"),
-                                             ("cfg5", "complex32")])
+                                             ("cfg5", "complex32"), ("cfg1", "complex64")])
 def test_bench_batch_rows_vs_oracle(oracle_lib, torch_dev, config, in_dtype):
     torch, dev = torch_dev
     from pypanadapter_amd import ZoomFFT
@@ -42,7 +42,9 @@ def test_bench_batch_rows_vs_oracle(oracle_lib, torch_dev, config, in_dtype):
         plan.process_device(xe.data_ptr(), L, F, rows.data_ptr(), st.cuda_stream)
         torch.cuda.synchronize()
         names = plan.launch_names()
-    assert names[0] in ("xa_stage_mix", "pc_fir", "pc_walk"), names  # the schedule the bench times
+    assert names[0] in ("xa_stage_mix", "pc_fir", "pc_walk", "pc_walk4"), names  # the schedule the bench times
+    if config == "cfg1":
+        assert names[0] == "xa_stage_mix", names  # zoom 4 at F = 4096: XA (the zoom-4 walk is slower)
     host = rows.cpu().numpy()
     assert np.isfinite(host).all()
     for f in PICK(F):

@@ -156,10 +156,11 @@ def test_pc_matches_xa_and_exact_rows(oracle_lib):
 def test_pc_refuses_outside_its_domain(path):
     from pypanadapter_amd import ZoomFFT
     x = np.zeros(299008, np.complex64)
-    with ZoomFFT(4096, 4, 2.4e6) as plan:
-        plan.set_path(path)
-        with pytest.raises(NotImplementedError):
-            plan.rows(x)
+    for zoom in ((2, 4) if path == 4 else (2, 16)):  # zoom 4 has the walk (path 5) only
+        with ZoomFFT(4096, zoom, 2.4e6) as plan:
+            plan.set_path(path)
+            with pytest.raises(NotImplementedError):
+                plan.rows(x)
     with ZoomFFT(1024, 8, 2.4e6) as plan:
         plan.set_path(path)
         with pytest.raises(NotImplementedError):
@@ -217,3 +218,96 @@ def test_pc_ragged_lengths_on_a_caller_stream(oracle_lib, zfft_lib, path):
         got = rows[L].cpu().numpy()
         for f in range(F):
             assert_row_close(got[f], oracle_lib.psd_row(xs[L][f], 2.4e6, N, 8, W), f"L={L} frame {f}")
+
+
+# ---- zoom 4: the walk (pc_walk_kernel<4>, path 5; automatic from 2048 frames) ----
+
+PC4_LENGTHS = [16384, 16385, 16386, 16387, 2048 * 9 + 3, 262144, 262144 + 2, 299008 + 1]
+
+
+@pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
+def test_pc4_decimate_vs_oracle(oracle_lib, flip):
+    """Zoom 4's two-stage cascade (cfg1's decimator, S:2096-2098 at fft_ratio 4) at every
+    L mod 4, against the float64 oracle of decimate(x, 2) twice."""
+    from pypanadapter_amd import ZoomFFT
+    rng = np.random.default_rng(4800 + flip)
+    for L in PC4_LENGTHS:
+        x = (rng.standard_normal(L) + 1j * rng.standard_normal(L)).astype(np.complex64)
+        x += np.exp(2j * np.pi * 0.013 * np.arange(L)).astype(np.complex64)
+        with ZoomFFT(1024, 4, 2.4e6, flip=flip) as plan:
+            plan.set_path(5)
+            d = plan.decimate(x)
+        ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 4, 2.4e6)
+        assert d.shape == ref.shape, (L, d.shape, ref.shape)
+        err = np.abs(d - ref) / np.abs(ref).max()
+        assert err.max() < PC_TOL, (L, flip, float(err.max()), int(err.argmax()), len(d))
+
+
+@pytest.mark.parametrize("N,L,F", [(1024, 262144, 5), (4096, 299008, 3), (2048, 131072 + 3, 4)])
+def test_pc4_rows_vs_oracle(oracle_lib, N, L, F):
+    from pypanadapter_amd import ZoomFFT
+    W = N // 4
+    x = _frames(F, L, N, 4, W, seed0=8100 + N // 1024)
+    with ZoomFFT(N, 4, 2.4e6, n_win=W) as plan:
+        plan.set_path(5)
+        rows = plan.rows(x)
+    for f in range(F):
+        assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, 4, W), f"N={N} L={L} frame {f}")
+
+
+def test_pc4_golden_rows():
+    """Every zoom-4 golden row the reference recorded whose frame the PC walk takes."""
+    from pypanadapter_amd import ZoomFFT
+    from conftest import window_of
+    n = 0
+    for c in golden_cases()["cases"]:
+        if c["zoom"] != 4 or c["n_samples"] < 16384:
+            continue
+        x = case_input(c)
+        with ZoomFFT(c["n_fft"], 4, c["fs"], n_win=c["n_win"], window=window_of(c["window"]),
+                     f_lo=c["f_lo"]) as plan:
+            plan.set_path(5)
+            row = plan.rows(x)
+        assert_row_close(row, golden_rows()[c["name"]], c["name"])
+        n += 1
+    assert n >= 1
+
+
+@pytest.mark.parametrize("fmt", ["complex32", "cu8", "f32"])
+def test_pc4_input_formats_and_lo(oracle_lib, fmt):
+    """Raw-source formats, np.flip and per-frame LOs through the zoom-4 walk."""
+    from pypanadapter_amd import ZoomFFT
+    F, L, N = 3, 262144 + 1, 1024
+    f_lo = [1.0, 150e3 + 1.0, -300e3 + 1.0]
+    x = np.stack([_frames(1, L, N, 4, 256, seed0=8300 + f, f_lo=f_lo[f])[0] for f in range(F)])
+    arr, vals = _encode(x, fmt)
+    with ZoomFFT(N, 4, 2.4e6, n_win=256, in_dtype=fmt, flip=True) as plan:
+        plan.set_path(5)
+        plan.set_lo_frames(f_lo, 1)
+        rows = plan.rows(arr)
+    for f in range(F):
+        assert_row_close(rows[f], oracle_lib.psd_row(vals[f, ::-1], 2.4e6, N, 4, 256, f_lo=f_lo[f]),
+                         f"{fmt} frame {f}")
+
+
+def test_pc4_size_independent_properties():
+    """Determinism, frame-order equivariance, exact x2 scaling, and the walk against the XA
+    schedule on the same batch."""
+    from pypanadapter_amd import ZoomFFT
+    x = _frames(8, 262144, 1024, 4, 256, seed0=8500)
+    with ZoomFFT(1024, 4, 2.4e6) as plan:
+        plan.set_path(5)
+        a = plan.rows(x)
+        b = plan.rows(x)
+        perm = np.random.default_rng(2).permutation(8)
+        c = plan.rows(x[perm])
+        d = plan.rows(2 * x)
+        da = plan.decimate(x[3])
+        plan.set_path(3)
+        xa = plan.rows(x)
+        dx = plan.decimate(x[3])
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(c, a[perm])
+    np.testing.assert_allclose(d - a, 20 * np.log10(4.0), atol=2e-4)
+    assert np.abs(da - dx).max() / np.abs(dx).max() < 2 * PC_TOL
+    np.testing.assert_allclose(xa, a, atol=2e-3)

@@ -148,3 +148,81 @@ def test_pc_model_plus_edge_maps_is_reference_decimate(L):
     out[len(out) - CR.shape[0]:] += (CR @ x[::-1][:CR.shape[1]])[::-1]
     err = np.abs(out - ref).max() / np.abs(ref).max()
     assert err < 2e-7, err             # fp32 storage of the rank-~10 maps
+
+
+# ---- zoom 4 (two stages; PcTab4, pc_walk_kernel<4>) ----
+
+def _model4():
+    s = _secs()
+    n9 = SOS[0, 0] * np.array([1, 8, 28, 56, 70, 56, 28, 8, 1.0])
+    f0 = _conv(n9, _neg(_poly(*s[0], range(4))))
+    f1 = _conv(n9, _neg(_poly(*s[1], range(4))), _neg(_poly(*s[0], [0, 1])))
+    g = [np.convolve(f, f[::-1]) for f in (f0, f1)]
+    own = [(s[0][0][i], s[0][1][i]) for i in (2, 3)]
+    ap = [(s[2][0][i], s[2][1][i]) for i in range(4)] + [(s[1][0][i], s[1][1][i]) for i in (0, 1)]
+    return g, own, ap
+
+
+def _run_model4(x, g, own, ap):
+    pad = 4096
+    y = np.concatenate([np.zeros(pad), x, np.zeros(pad)])
+    for r in range(2):
+        if r == 1:
+            so = np.array([[1, 0, 0, 1, a1, a2] for a1, a2 in own])
+            y = ss.sosfilt(so, ss.sosfilt(so, y)[::-1])[::-1]
+        c = (len(g[r]) - 1) // 2
+        y = np.convolve(y, g[r])[c::2][:len(y) // 2]
+    sa = np.array([[1, 0, 0, 1, a1, a2] for a1, a2 in ap])
+    y = ss.sosfilt(sa, ss.sosfilt(sa, y)[::-1])[::-1]
+    n2 = (len(x) + 1) // 2
+    n2 = (n2 + 1) // 2
+    return y[pad // 4:pad // 4 + n2]
+
+
+def _edge4(side, lm, shipped=False):
+    if shipped:
+        v = _call(14, 0 if side == 0 else 1 + lm)
+        R, J, r = int(v[0]), int(v[1]), int(v[2])
+        return v[3:3 + R * r].reshape(R, r), v[3 + R * r:3 + R * r + J * r].reshape(r, J).T
+    v = _call(12 + side, lm)
+    R, J, r = int(v[0]), int(v[1]), int(v[2])
+    return v[3:3 + R * r].reshape(R, r), v[3 + R * r:3 + R * r + J * r].reshape(J, r)
+
+
+def test_pc4_fir_taps_match_polyphase_factorisation():
+    g, _, _ = _model4()
+    taps = _call(5)
+    want = np.concatenate(g)
+    assert taps.size == want.size == 33 + 41
+    np.testing.assert_allclose(taps, want, rtol=0, atol=4e-8 * np.abs(want).max())
+
+
+@pytest.mark.parametrize("side,lm", [(0, 0)] + [(1, k) for k in range(4)])
+def test_pc4_shipped_edge_maps_are_the_builders(side, lm):
+    Ub, Vb = _edge4(side, lm)
+    Us, Vs = _edge4(side, lm, shipped=True)
+    assert Ub.shape == Us.shape and Vb.shape == Vs.shape
+    np.testing.assert_array_equal(Us, Ub)
+    np.testing.assert_array_equal(Vs, Vb)
+
+
+@pytest.mark.parametrize("L", [16384, 16385, 16386, 16387, 20006, 262144 + 1])
+def test_pc4_model_plus_edge_maps_is_reference_decimate(L):
+    """Zoom 4 (cfg1): the two-stage model and its shipped frame-end maps give scipy's
+    decimate(decimate(x, 2), 2) -- the reference's zoomfft at ratio 4 -- for every L mod 4."""
+    g, own, ap = _model4()
+    rng = np.random.default_rng(L + 4)
+    x = rng.standard_normal(L) + 1j * rng.standard_normal(L)
+    x += 3 * np.exp(2j * np.pi * 0.027 * np.arange(L))
+    ref = ss.decimate(ss.decimate(x, 2), 2)
+    out = _run_model4(x, g, own, ap)
+    assert out.shape == ref.shape
+    inner = np.abs(out - ref)[300:-300].max() / np.abs(ref).max()
+    assert inner < 1e-12, inner
+    UL, VL = _edge4(0, L % 4, shipped=True)
+    UR, VR = _edge4(1, L % 4, shipped=True)
+    CL, CR = UL @ VL.T, UR @ VR.T
+    out[:CL.shape[0]] += CL @ x[:CL.shape[1]]
+    out[len(out) - CR.shape[0]:] += (CR @ x[::-1][:CR.shape[1]])[::-1]
+    err = np.abs(out - ref).max() / np.abs(ref).max()
+    assert err < 2e-7, err

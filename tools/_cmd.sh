@@ -1,21 +1,14 @@
 # Scratch GPU command of the current session (run as: gpurun -- 'bash tools/_cmd.sh').
 set -u
 export TMPDIR=/tmp
-V=pypanadapter_amd/lib/variants
-O=gpurun_out/r05g; mkdir -p $O
-run() {  # name lib path
-  if [ "$2" = default ]; then unset ZFFT_LIB_PATH; else export ZFFT_LIB_PATH=$2; fi
-  timeout -k 10 300 python bench.py --steps 100 --warmup 3 --no-cpu --no-e2e --no-check --path $3 > $O/$1.log 2>&1 || exit $?
-  python3 -c "import json; d=json.loads([l for l in open('$O/$1.log') if l.startswith('{')][0]); print('$1', d['ms_per_step'], d['kernels'])"
-}
+O=gpurun_out/r05h; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_pc.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread -k "pc4" > $O/pytest_pc4.log 2>&1; rc=$?
+tail -15 $O/pytest_pc4.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+[ $rc -eq 0 ] || exit 0
 for rep in 1 2; do
-  run p5_$rep default 5
-  run p6_$rep default 6
-  run p6cp1_$rep $V/libzfft_sp_cp1.so 6
-  run p6cp2_$rep $V/libzfft_sp_cp2.so 6
-  run p6dppcp2_$rep $V/libzfft_sp_dpp4cp2.so 6
+  for p in 3 5; do
+    timeout -k 10 300 python bench.py --config cfg1 --steps 50 --warmup 2 --no-cpu --no-e2e --path $p > $O/cfg1_p${p}_$rep.log 2>&1 || exit $?
+    python3 -c "import json; d=json.loads([l for l in open('$O/cfg1_p${p}_$rep.log') if l.startswith('{')][0]); print('cfg1 path $p', d['ms_per_step'], d['kernels'], d.get('parity_checked_frames'))"
+  done
 done
-run p6ko16 $V/libzfft_ko16.so 6
-run p6ko7 $V/libzfft_ko7.so 6
-run p5ko16 $V/libzfft_ko16.so 5
-run p5ko7 $V/libzfft_ko7.so 5
