@@ -53,6 +53,12 @@ constexpr int kKo = 0;
 #ifndef PC_PRIO
 #define PC_PRIO 0
 #endif
+#if !ZFFT_DIAG && defined(PC_ASMFMA)
+#error "PC_ASMFMA is a diagnostic knob: build with -DZFFT_DIAG"
+#endif
+#ifndef PC_ASMFMA
+#define PC_ASMFMA 0  // walk FIRs: taps as aligned SGPR pairs selected by op_sel (no s_mov)
+#endif
 
 namespace zfft {
 namespace pc {
@@ -97,6 +103,45 @@ __device__ __forceinline__ P fresh(P p) {
   return p;
 }
 __device__ __forceinline__ v2f lo2(v4f w) { return v2f{w.x, w.y}; }
+// acc += g[u] x0 (+ g[u + 1] x1): one FIR tap pair (u even) as an aligned SGPR pair, the tap
+// picked by op_sel -- the compiler's own form copies the odd tap into an even SGPR first
+typedef unsigned long long u64s;
+template <class TP>
+__device__ __forceinline__ u64s tap_pair(TP taps, int u) {
+  return *(const u64s __attribute__((address_space(4))) *)(taps + u);
+}
+__device__ __forceinline__ void fma_tap_lo(v2f &acc, u64s g, v2f x) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "s"(g), "v"(x));
+}
+__device__ __forceinline__ void fma_tap_hi(v2f &acc, u64s g, v2f x) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(g), "v"(x));
+}
+// acc + c[1] b + c[0] a (inner product first, as vfma(c0, a, vfma(c1, b, acc))), c an aligned
+// coefficient pair of the section tables
+template <class PP>
+__device__ __forceinline__ v2f fma2(PP c, v2f a, v2f b, v2f acc) {
+  if constexpr (PC_ASMFMA) {
+    const u64s g = tap_pair(c, 0);
+    fma_tap_hi(acc, g, b);
+    fma_tap_lo(acc, g, a);
+    return acc;
+  } else {
+    return vfma(splat(c[0]), a, vfma(splat(c[1]), b, acc));
+  }
+}
+template <int G, class TP>
+__device__ __forceinline__ void fir_pair(v2f &acc, TP taps, int u, v2f x0, v2f x1) {
+  if constexpr (PC_ASMFMA) {
+    if (u >= 0 && u < G) {
+      const u64s g = tap_pair(taps, u);
+      fma_tap_lo(acc, g, x0);
+      if (u + 1 < G) fma_tap_hi(acc, g, x1);
+    }
+  } else {
+    if (u >= 0 && u < G) acc = vfma(splat(taps[u]), x0, acc);
+    if (u + 1 >= 0 && u + 1 < G) acc = vfma(splat(taps[u + 1]), x1, acc);
+  }
+}
 // lane k's v of a wave, for a wave-uniform k (v_readlane: an SGPR pair, no memory round trip)
 __device__ __forceinline__ v2f lane_val(v2f v, int k) {
   return v2f{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), k)),
@@ -320,8 +365,8 @@ __device__ __forceinline__ void sec_block(v2f (&v)[B], CT tab0, LP scr, int lane
     else if (d == 1) p0 = shiftk<UP, 2>(e0, lane), p1 = shiftk<UP, 2>(e1, lane);
     else if (d == 2) p0 = shiftk<UP, 4>(e0, lane), p1 = shiftk<UP, 4>(e1, lane);
     else p0 = shiftk<UP, 8>(e0, lane), p1 = shiftk<UP, 8>(e1, lane);
-    const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
-    e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
+    const v2f n0 = fma2(&S.pw[d][0], p0, p1, e0);
+    e1 = fma2(&S.pw[d][2], p0, p1, e1);
     e0 = n0;
   }
   v2f s0 = splat(0.f), s1 = splat(0.f);  // state entering this wave's first block
@@ -350,7 +395,7 @@ __device__ __forceinline__ void sec_block(v2f (&v)[B], CT tab0, LP scr, int lane
 #pragma unroll
   for (int c = 0; c < DCUT; ++c) {
     const int k = UP ? c : B - 1 - c;
-    v[k] = vfma(splat(S.ct[c][0]), i0, vfma(splat(S.ct[c][1]), i1, v[k]));
+    v[k] = fma2(&S.ct[c][0], i0, i1, v[k]);
   }
 }
 
@@ -380,8 +425,8 @@ __device__ __forceinline__ void sec_run(v2f (&v)[B], CS S, int lane) {
     else if (d == 1) p0 = shiftk<UP, 2>(e0, lane), p1 = shiftk<UP, 2>(e1, lane);
     else if (d == 2) p0 = shiftk<UP, 4>(e0, lane), p1 = shiftk<UP, 4>(e1, lane);
     else p0 = shiftk<UP, 8>(e0, lane), p1 = shiftk<UP, 8>(e1, lane);
-    const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
-    e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
+    const v2f n0 = fma2(&S.pw[d][0], p0, p1, e0);
+    e1 = fma2(&S.pw[d][2], p0, p1, e1);
     e0 = n0;
   }
   v2f i0 = wshift<UP>(e0), i1 = wshift<UP>(e1);
@@ -389,7 +434,7 @@ __device__ __forceinline__ void sec_run(v2f (&v)[B], CS S, int lane) {
 #pragma unroll
   for (int c = 0; c < DCUT; ++c) {
     const int k = UP ? c : B - 1 - c;
-    v[k] = vfma(splat(S.ct[c][0]), i0, vfma(splat(S.ct[c][1]), i1, v[k]));
+    v[k] = fma2(&S.ct[c][0], i0, i1, v[k]);
   }
 }
 template <int S, bool UP>
@@ -518,8 +563,8 @@ __device__ __forceinline__ void wsec(v2f (&v)[B], TP tab0, LP scr, int lane, int
     else if (d == 2) p0 = shiftk<UP, 4>(e0, lane), p1 = shiftk<UP, 4>(e1, lane);
     else if (d == 3) p0 = shiftk<UP, 8>(e0, lane), p1 = shiftk<UP, 8>(e1, lane);
     else p0 = shiftk<UP, 16>(e0, lane), p1 = shiftk<UP, 16>(e1, lane);
-    const v2f n0 = vfma(splat(S.pw[d][0]), p0, vfma(splat(S.pw[d][1]), p1, e0));
-    e1 = vfma(splat(S.pw[d][2]), p0, vfma(splat(S.pw[d][3]), p1, e1));
+    const v2f n0 = fma2(&S.pw[d][0], p0, p1, e0);
+    e1 = fma2(&S.pw[d][2], p0, p1, e1);
     e0 = n0;
   }
   if (lane == (UP ? 63 : 0)) {
@@ -548,7 +593,7 @@ __device__ __forceinline__ void wsec(v2f (&v)[B], TP tab0, LP scr, int lane, int
 #pragma unroll
   for (int c = 0; c < B; ++c) {
     const int k = UP ? c : B - 1 - c;
-    v[k] = vfma(splat(S.ct[c][0]), i0, vfma(splat(S.ct[c][1]), i1, v[k]));
+    v[k] = fma2(&S.ct[c][0], i0, i1, v[k]);
   }
 }
 
@@ -673,11 +718,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
           const v4f w = *(LP4)(xb + (j >> 4) * kXRow + (j & 15));
           const v2f x0 = lo2(w), x1 = hi2(w);
 #pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const int u = j - 2 * r;
-            if (u >= 0 && u < kPcG0) acc[r] = vfma(splat(tab->g0[u]), x0, acc[r]);
-            if (u + 1 >= 0 && u + 1 < kPcG0) acc[r] = vfma(splat(tab->g0[u + 1]), x1, acc[r]);
-          }
+          for (int r = 0; r < 8; ++r) fir_pair<kPcG0>(acc[r], tab->g0, j - 2 * r, x0, x1);
         }
       }
       if constexpr (!(kKo & 128)) __syncthreads();
@@ -706,11 +747,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
           const v4f w = *(LP4)(yb + (j >> 3) * kYRow + (j & 7));
           const v2f x0 = lo2(w), x1 = hi2(w);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int u = j - 2 * r;
-            if (u >= 0 && u < kPcG1) b[r] = vfma(splat(tab->g1[u]), x0, b[r]);
-            if (u + 1 >= 0 && u + 1 < kPcG1) b[r] = vfma(splat(tab->g1[u + 1]), x1, b[r]);
-          }
+          for (int r = 0; r < 4; ++r) fir_pair<kPcG1>(b[r], tab->g1, j - 2 * r, x0, x1);
         }
         const LP zo = zl + zp(kPcWQ * (1 + c) + 4 * t);
         *(LP4)zo = cat(b[0], b[1]);
@@ -790,11 +827,7 @@ __global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, 
         const v4f w = *(LP4)(zb + j);
         const v2f x0 = lo2(w), x1 = hi2(w);
 #pragma unroll
-        for (int r = 0; r < 9; ++r) {
-          const int q = j - 2 * r;
-          if (q >= 0 && q < G) u[r] = vfma(splat(taps()[q]), x0, u[r]);
-          if (q + 1 >= 0 && q + 1 < G) u[r] = vfma(splat(taps()[q + 1]), x1, u[r]);
-        }
+        for (int r = 0; r < 9; ++r) fir_pair<G>(u[r], taps(), j - 2 * r, x0, x1);
       }
 #pragma unroll
       for (int r = 0; r < 9; ++r) xl[9 * t + r] = u[r];
