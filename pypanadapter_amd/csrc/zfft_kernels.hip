@@ -741,9 +741,15 @@ __global__ __launch_bounds__(MAXT, 1) void welch_rows_kernel(const v2f *__restri
 #ifndef ZFFT_DIF_PP
 #define ZFFT_DIF_PP 1   // two prefetch arrays used in turn, N < 16384 (0: one, copied into v
 #endif                  // each segment): cfg2 Welch 0.486 -> 0.46 ms (profiles/r03_ab/r03dpp)
-constexpr int kDifPf = 16;             // values per thread prefetched a segment ahead (N = 4096)
+#ifndef ZFFT_DIF_PF4K
+#define ZFFT_DIF_PF4K 16
+#endif
+#ifndef ZFFT_DIF_WAVES4K
+#define ZFFT_DIF_WAVES4K 3
+#endif
+constexpr int kDifPf = ZFFT_DIF_PF4K;  // values per thread prefetched a segment ahead (N = 4096)
 constexpr int kDifPfSmall = 8;         // the same for N <= 2048
-constexpr int kDifWaves = 3;           // waves per SIMD the registers are cut for (PRUNE, N = 4096)
+constexpr int kDifWaves = ZFFT_DIF_WAVES4K;  // waves per SIMD the registers are cut for (PRUNE, N = 4096)
 constexpr int kDifWavesSmall = 3;      // the same for N <= 2048 (full form)
 constexpr int kDifWavesSmallPrune = 4; // N <= 2048, PRUNE: 4 waves/SIMD (cfg1: 4096 one-wave
                                        // frames fill the GPU's 4096 slots in one round)

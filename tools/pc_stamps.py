@@ -39,9 +39,9 @@ def main():
     assert rc == 0, rc
     v = np.array(list(buf), dtype=np.float64)
     n = len(SEGS)
-    wave_tiles = v[n] * 4  # four waves per workgroup
+    wave_tiles = v[n]  # every wave's lane 0 adds its tile count
     tot = v[:n].sum()
-    print(f"frames {F}  workgroup tiles {v[n]:.0f}  cycles per wave and tile {tot / wave_tiles:.0f}")
+    print(f"frames {F}  wave tiles {v[n]:.0f}  cycles per wave and tile {tot / wave_tiles:.0f}")
     for name, c in zip(SEGS, v[:n]):
         print(f"  {name:24s} {c / wave_tiles:8.0f} cyc  {100 * c / tot:5.1f} %")
 
