@@ -398,6 +398,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per rank (default: config)")
+    ap.add_argument("--zoom", type=int, default=0, help="override the config's zoom (not a BASELINE line)")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--warm", type=int, default=0)
     ap.add_argument("--path", type=int, default=0,
@@ -420,6 +421,9 @@ def main():
         sys.exit(spawn_ranks(args))
 
     cfg = dict(CONFIGS[args.config])
+    if args.zoom:  # e.g. the PC head + XA tail at zoom 16 on cfg2's frames
+        cfg["zoom"] = args.zoom
+        cfg["desc"] += f" (zoom overridden to {args.zoom}: not a BASELINE config)"
     F = args.frames or cfg["frames"]
     N, zoom, fs = cfg["n_fft"], cfg["zoom"], cfg["fs"]
     L = N * cfg["n_avg"]

@@ -59,6 +59,15 @@ constexpr int kKo = 0;
 #ifndef PC_ASMFMA
 #define PC_ASMFMA 0  // walk FIRs: taps as aligned SGPR pairs selected by op_sel (no s_mov)
 #endif
+// PC_OCC3 (diagnostic builds only, timing-only: the LDS regions race by design): the walk at
+// three workgroups per CU -- the own-rate span aliases the input tile (LDS 81 -> 45 KB) and the
+// kernel is compiled for 3 waves per SIMD (<= 168 VGPRs, spilling what does not fit)
+#if !ZFFT_DIAG && defined(PC_OCC3)
+#error "PC_OCC3 is a diagnostic knob: build with -DZFFT_DIAG"
+#endif
+#ifndef PC_OCC3
+#define PC_OCC3 0
+#endif
 
 namespace zfft {
 namespace pc {
@@ -633,11 +642,19 @@ template <> struct WalkZ<4> {
   static __device__ __forceinline__ int64_t xs_of(int g) { return 2 * (2 * (int64_t)WM0 + 720 + 2048 * (int64_t)g) - 16; }
 };
 template <int DT, int FLIP, int ZOOM>
-__global__ void __launch_bounds__(256) pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3,
-                                                      typename WalkZ<ZOOM>::Tab tab) {
+__global__ void __launch_bounds__(256)
+#if PC_OCC3
+__attribute__((amdgpu_waves_per_eu(3)))
+#endif
+pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, typename WalkZ<ZOOM>::Tab tab) {
   using Z = WalkZ<ZOOM>;
+#if PC_OCC3
+  __shared__ v4f xl4[(kWZP > kXRows * kXRow ? kWZP : kXRows * kXRow) / 2];
+  v4f __attribute__((address_space(3))) *z4 = (v4f __attribute__((address_space(3))) *)xl4;
+#else
   __shared__ v4f xl4[kXRows * kXRow / 2];  // K1 input tile, then y1; then u3 + staged outputs
   __shared__ v4f z4[kWZP / 2];             // own-rate samples, span s in [256, 5376)
+#endif
   __shared__ v4f scr4[16];                 // cross-wave states (4 section calls)
   __shared__ v4f car4[2];                  // causal sections' carried states
   __shared__ v4f y1c4[24];                 // the 48 y1 two sub-tiles share

@@ -796,6 +796,12 @@ bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
 bool pc4_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == 2 && L >= kPcMinL && frames <= 65535;
 }
+// Zoom >= 16: PC takes the first three stages (decimate x 3 exactly, frame-end maps included)
+// and XA the remaining K - 3 on its 1/8-rate output -- the reference's stages are applied one
+// after another (S:2096-2098), so the composition is the same cascade.
+bool pc_head_fits(const zfft_plan *p, int64_t L, int frames) {
+  return p->K > kPcStages && L >= kPcMinL && frames <= 65535;
+}
 
 // Host copy of the PC tables: built once per process (fp64, microseconds); the frame-end maps
 // are the constants of pc_edge_maps.h (tools/gen_pc_edge.py).
@@ -840,14 +846,15 @@ int ensure_pc(zfft_plan *p) {
 
 // PC path: K1 (FIRs) -> y2 (ping) -> K2 (own-rate sections, FIR, output-rate sections) ->
 // out (pong) -> K3 (frame-end maps, in place).
+// K = the stages PC runs: p->K (zoom 4 or 8), or 3 as the head of a longer cascade.
 int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vector<int64_t> &n,
-           bool walk, const float2 **out, hipStream_t st) {
+           bool walk, const float2 **out, hipStream_t st, int K) {
   int rc = ensure_pc(p);
   if (rc) return rc;
-  const int64_t n3 = n[p->K];
+  const int64_t n3 = n[K];
   const PcTab *tab = p->pc_tab.as<PcTab>();
   hipError_t e;
-  if (p->K == 2) {  // zoom 4: the walk only
+  if (K == 2) {  // zoom 4: the walk only
     e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
     e = launch_pc_walk4(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab4.as<PcTab4>(), st);
@@ -873,8 +880,8 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
   }
   // map 0 = frame start, 1 + (L mod 2^K) = frame end (pc_edge_maps.h)
   const float *eb = p->pc_edge.as<float>();
-  const PcEdgeConst &m0 = p->K == 2 ? kPcEdge4Idx[0] : kPcEdgeIdx[0];
-  const PcEdgeConst &m1 = p->K == 2 ? kPcEdge4Idx[1 + (L & 3)] : kPcEdgeIdx[1 + (L & 7)];
+  const PcEdgeConst &m0 = K == 2 ? kPcEdge4Idx[0] : kPcEdgeIdx[0];
+  const PcEdgeConst &m1 = K == 2 ? kPcEdge4Idx[1 + (L & 3)] : kPcEdgeIdx[1 + (L & 7)];
   const float *const U[2] = {eb + m0.u, eb + m1.u};
   const float *const V[2] = {eb + m0.v, eb + m1.v};
   const int R[2] = {m0.R, m1.R}, J[2] = {m0.J, m1.J}, r[2] = {m0.r, m1.r};
@@ -882,6 +889,26 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
   if (e != hipSuccess) return hip_fail(e, "pc_edge launch");
   mark(p, st, "pc_edge");
   *out = p->pong.as<float2>();
+  return ZFFT_OK;
+}
+
+// PC head (3 stages into pong) + XA for stages 3 .. K-1 (ping, pong, ... in turn; no LO mix).
+int run_pc_head(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vector<int64_t> &n,
+                bool walk, const float2 **out, hipStream_t st) {
+  const float2 *cur = nullptr;
+  int rc = run_pc(p, in, L, frames, n, walk, &cur, st, kPcStages);
+  if (rc) return rc;
+  hipError_t e = p->ping.ensure((size_t)frames * n[kPcStages + 1] * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+  for (int k = kPcStages; k < p->K; ++k) {
+    float2 *dst = ((k - kPcStages) & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
+    const InDesc src{cur, n[k], n[k], kInC64, 0};
+    e = launch_xa_stage(src, (int)n[k], p->lo.as<float2>(), false, dst, frames, p->xa_tab.as<XaTab>(), st);
+    if (e != hipSuccess) return hip_fail(e, "xa_stage launch");
+    mark(p, st, "xa_stage");
+    cur = dst;
+  }
+  *out = cur;
   return ZFFT_OK;
 }
 
@@ -894,16 +921,21 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  if ((p->path == 4 && !pc_fits(p, L, frames)) || (p->path == 5 && !pc_fits(p, L, frames) && !pc4_fits(p, L, frames)))
-    return fail(ZFFT_EUNSUPPORTED, "PC decimator needs zoom 8 (path 4, 5) or zoom 4 (path 5), frames "
-                                   "of >= 16384 samples and <= 65535 frames per call");
-  if (p->path == 5 && pc4_fits(p, L, frames)) return run_pc(p, in, L, frames, n, true, out, st);
+  const bool pc8 = pc_fits(p, L, frames), head = pc_head_fits(p, L, frames);
+  if ((p->path == 4 && !pc8 && !head) || (p->path == 5 && !pc8 && !head && !pc4_fits(p, L, frames)))
+    return fail(ZFFT_EUNSUPPORTED, "PC decimator needs zoom >= 8 (path 4, 5) or zoom 4 (path 5), "
+                                   "frames of >= 16384 samples and <= 65535 frames per call");
+  if (p->path == 5 && pc4_fits(p, L, frames)) return run_pc(p, in, L, frames, n, true, out, st, p->K);
+  const bool walk = p->path == 5 || (p->path == 0 && frames >= kPcWalkMinFrames);
   // PC is the fastest schedule wherever it applies, from one frame per call (the
   // reference's use: 0.083 against 0.37 ms for path 1) to full batches (1024 frames: 1.44
   // against 2.03 ms for XA) -- tools/sweep_schedule.py, profiles/r04l
-  if (p->path == 4 || p->path == 5 || (p->path == 0 && pc_fits(p, L, frames)))
-    return run_pc(p, in, L, frames, n, p->path == 5 || (p->path == 0 && frames >= kPcWalkMinFrames),
-                  out, st);
+  if (pc8 && (p->path == 0 || p->path == 4 || p->path == 5))
+    return run_pc(p, in, L, frames, n, walk, out, st, p->K);
+  // zoom >= 16: the head where XA would take the batch (its tail stages are XA's)
+  if (p->path == 4 || p->path == 5 ||
+      (p->path == 0 && head && auto_xa(frames, n[kPcStages]) && xa_fits(p, L)))
+    return run_pc_head(p, in, L, frames, n, walk, out, st);
   if (p->path == 3 || (p->path == 0 && auto_xa(frames, L) && xa_fits(p, L)))
     return run_xa(p, in, frames, n, out, st);
   if (use_fused(p, L, frames)) return run_fused(p, in, L, frames, n, out, st);

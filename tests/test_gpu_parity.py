@@ -409,13 +409,15 @@ def test_facade_matches_reference_rows():
                                         (8, 4095, 32768, "pc"), (8, 4, 8192, "exact"),
                                         (4, 1, 262144, "exact"), (4, 256, 262144, "exact"),
                                         (4, 384, 262144, "xa"), (4, 64, 1048576, "exact"),
-                                        (4, 128, 1048576, "fused"), (4, 768, 1048576, "xa")])
+                                        (4, 128, 1048576, "fused"), (4, 768, 1048576, "xa"),
+                                        (16, 384, 262144, "pc"), (16, 8, 262144, "exact")])
 def test_auto_schedule_by_batch(z, F, L, want):
     """The automatic decimator schedule follows the measured crossovers (zfft_plan.cpp
     pc_fits / kPcWalkMinFrames / auto_xa / use_fused, tools/sweep_schedule.py,
     profiles/r04l): at zoom 8 the PC polyphase cascade for every batch of frames >= 16384
     samples (one frame per call -- the reference's use -- included), as its walk kernel
-    from 4096 frames per call; elsewhere small batches run the exact blocked passes,
+    from 4096 frames per call; zoom >= 16 as PC's first three stages + XA where XA would take
+    the batch; elsewhere small batches run the exact blocked passes,
     batches of >= 2^27 samples the fused interior with edge windows, and >= 384 frames of
     <= 2^19 samples (768 of longer ones) the XA tiles."""
     import torch
@@ -423,7 +425,7 @@ def test_auto_schedule_by_batch(z, F, L, want):
     dev = torch.device("cuda", 0)
     x = torch.zeros((F, L, 2), dtype=torch.float32, device=dev)
     x[..., 0] = 1.0
-    N = 4096 if z == 8 else 1024
+    N = {4: 1024, 8: 4096, 16: 4096}[z]
     rows = torch.empty((F, N // z), dtype=torch.float32, device=dev)
     with ZoomFFT(N, z, 2.4e6, n_win=N // z) as plan:
         plan.set_timing(True)
@@ -434,6 +436,8 @@ def test_auto_schedule_by_batch(z, F, L, want):
              "xa": ("xa_stage_mix",), "pc": ("pc_fir",), "walk": ("pc_walk",)}[want]
     assert names[0] in first, names
     assert ("edge_windows" in names) == (want == "fused"), names
+    if z == 16:  # the PC head's tail stage
+        assert ("xa_stage" in names) == (want == "pc"), names
     del x, rows
     torch.cuda.empty_cache()
 

@@ -156,7 +156,7 @@ def test_pc_matches_xa_and_exact_rows(oracle_lib):
 def test_pc_refuses_outside_its_domain(path):
     from pypanadapter_amd import ZoomFFT
     x = np.zeros(299008, np.complex64)
-    for zoom in ((2, 4) if path == 4 else (2, 16)):  # zoom 4 has the walk (path 5) only
+    for zoom in ((2, 4) if path == 4 else (2,)):  # zoom 4 has the walk (path 5) only
         with ZoomFFT(4096, zoom, 2.4e6) as plan:
             plan.set_path(path)
             with pytest.raises(NotImplementedError):
@@ -218,6 +218,67 @@ def test_pc_ragged_lengths_on_a_caller_stream(oracle_lib, zfft_lib, path):
         got = rows[L].cpu().numpy()
         for f in range(F):
             assert_row_close(got[f], oracle_lib.psd_row(xs[L][f], 2.4e6, N, 8, W), f"L={L} frame {f}")
+
+
+# ---- zoom >= 16: PC for the first three stages, XA for the rest (run_pc_head) ----
+
+@pytest.mark.parametrize("zoom", [16, 32])
+@pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
+@PC_PATHS
+def test_pc_head_decimate_vs_oracle(oracle_lib, zoom, flip, path):
+    """decimate(x, 2) x log2(zoom) as PC's exact x8 (frame-end maps at every L mod 8) followed
+    by XA's stages on its output, against the float64 oracle; XA's 1e-5 per stage on top."""
+    from pypanadapter_amd import ZoomFFT
+    rng = np.random.default_rng(4600 + zoom + flip)
+    for L in [16384, 16387, 16390, 3968 * 5 + 1, 262144 + 5, 299008]:
+        x = (rng.standard_normal(L) + 1j * rng.standard_normal(L)).astype(np.complex64)
+        x += np.exp(2j * np.pi * 0.0023 * np.arange(L)).astype(np.complex64)
+        with ZoomFFT(4096, zoom, 2.4e6, flip=flip) as plan:
+            plan.set_path(path)
+            plan.set_timing(True)
+            d = plan.decimate(x)
+            names = plan.launch_names()
+        assert names.count("xa_stage") == {16: 1, 32: 2}[zoom], names
+        ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, zoom, 2.4e6)
+        assert d.shape == ref.shape, (L, d.shape, ref.shape)
+        err = np.abs(d - ref) / np.abs(ref).max()
+        assert err.max() < 2 * PC_TOL, (L, zoom, flip, float(err.max()), int(err.argmax()), len(d))
+
+
+@PC_PATHS
+def test_pc_head_golden_rows(path):
+    """Every golden row the reference recorded at zoom >= 16 whose frame PC takes."""
+    from pypanadapter_amd import ZoomFFT
+    from conftest import window_of
+    n = 0
+    for c in golden_cases()["cases"]:
+        if c["zoom"] < 16 or c["n_samples"] < 16384:
+            continue
+        x = case_input(c)
+        with ZoomFFT(c["n_fft"], c["zoom"], c["fs"], n_win=c["n_win"], window=window_of(c["window"]),
+                     f_lo=c["f_lo"]) as plan:
+            plan.set_path(path)
+            row = plan.rows(x)
+        assert_row_close(row, golden_rows()[c["name"]], c["name"])
+        n += 1
+    assert n >= 3
+
+
+def test_pc_head_auto_batch_rows(oracle_lib):
+    """At a batch XA would take (384 frames), zoom 16 runs the PC head + one XA stage on its
+    own; rows of three frames against the oracle."""
+    from pypanadapter_amd import ZoomFFT
+    F, L, N = 384, 65536 + 3, 2048
+    x = np.zeros((F, L), np.complex64)
+    for f in (0, 191, F - 1):
+        x[f] = _frames(1, L, N, 16, 128, seed0=7900 + f)[0]
+    with ZoomFFT(N, 16, 2.4e6, n_win=128) as plan:
+        plan.set_timing(True)
+        rows = plan.rows(x)
+        names = plan.launch_names()
+    assert names[0] == "pc_fir" and "xa_stage" in names and "pc_edge" in names, names
+    for f in (0, 191, F - 1):
+        assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, 16, 128), f"frame {f}")
 
 
 # ---- zoom 4: the walk (pc_walk_kernel<4>, path 5; automatic from 2048 frames) ----
