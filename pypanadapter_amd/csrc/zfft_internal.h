@@ -239,7 +239,15 @@ struct WelchGeom {
   // four-step only: the column pass leaves per-column-group partial sums of each segment and
   // the row pass subtracts mean * FFT(window) after the transform (nperseg == n_fft)
   int fused_mean = 0;
+  // in-place DIF only: each frame's segments split over `split` workgroups (few frames per
+  // call), their linear partial PSDs in parts[(f split + part) n_win + j], summed in part
+  // order and converted to dB by a second launch (split 1: the row directly)
+  int split = 1;
+  float *parts = nullptr;
 };
+// DIF Welch split for a call of `frames` frames: enough workgroups for the chip (about 768 at
+// N = 4096), at least two segments each; 1 for full batches.
+int welch_dif_split(int n_fft, int nseg, int frames);
 
 hipError_t launch_welch_rows(const float2 *x, int64_t len, const float *win, const float2 *tw,
                              const WelchGeom &g, float *rows, int frames, hipStream_t st);
@@ -265,6 +273,7 @@ hipError_t launch_autolevel_hist_hi(const float *ring, int64_t n, unsigned *hist
 hipError_t launch_autolevel_hist_lo(const float *ring, int64_t n, const unsigned *bins, int nbins,
                                     unsigned *hist, hipStream_t st);
 // out[f][i] = in(f, i) (* lo[i] when lo) as complex64, natural layout, frames x len.
+hipError_t launch_fill_c64(float2 *out, int64_t n, float re, float im, hipStream_t st);
 hipError_t launch_ingest(const InDesc &in, const float2 *lo, float2 *out, int frames,
                          hipStream_t st);
 

@@ -871,8 +871,11 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
   constexpr int PFN = PF > 0 ? PF : 1;
   v2f pfa[PFN], pfb[PFN];  // ping-pong prefetch: segment s's values arrive in one, s+1's in
                            // the other (a single array was copied into v every segment)
-  load_seg(pfa, 0, threadIdx.x % T);
-  post_sum(pfa, 0, 0, threadIdx.x % T);
+  // this workgroup's segments [s0, s1): all of them, or part blockIdx.y of g.split
+  const int per = (g.nseg + g.split - 1) / g.split;
+  const int s0 = (int)blockIdx.y * per, s1 = min(g.nseg, s0 + per);
+  load_seg(pfa, s0, threadIdx.x % T);
+  post_sum(pfa, s0 & 1, s0, threadIdx.x % T);
   sync();
   constexpr int NACC = PRUNE ? 2 * (16 / D::RL) : 16;
   float acc[NACC];
@@ -894,7 +897,7 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = r < PF ? pf[r] : DIF_X(s, t, r);
     }
-    const bool more = s + 1 < g.nseg;
+    const bool more = s + 1 < s1;
     // (addresses from the loop-invariant thread id: computed once, outside the loop)
     if (more) {  // in flight during this segment's transform
       if (2 * g.step == N) {
@@ -971,30 +974,45 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
     sync();  // last-stage reads done before the next segment's stage-1 stores
     };
   if constexpr (ZFFT_DIF_PP && N != 16384) {  // N = 16384 (4-value prefetch): one array
-    for (int s = 0; s < g.nseg; s += 2) {      // measured faster (0.69 vs 0.78 ms at cfg3)
+    for (int s = s0; s < s1; s += 2) {         // measured faster (0.69 vs 0.78 ms at cfg3)
       seg_step(s, pfa, pfb);
-      if (s + 1 < g.nseg) seg_step(s + 1, pfb, pfa);
+      if (s + 1 < s1) seg_step(s + 1, pfb, pfa);
     }
   } else {
     (void)pfb;
-    for (int s = 0; s < g.nseg; ++s) seg_step(s, pfa, pfa);
+    for (int s = s0; s < s1; ++s) seg_step(s, pfa, pfa);
   }
   const int t = threadIdx.x % T;
-  float *__restrict__ row = rows + (int64_t)f * g.n_win;
   if (!owner) return;
+  float *__restrict__ row = g.split > 1 ? g.parts + ((int64_t)f * g.split + blockIdx.y) * g.n_win
+                                        : rows + (int64_t)f * g.n_win;
 #pragma unroll
   for (int i = 0; i < NACC; ++i) {
     const int q = PRUNE ? 16 * t + D::RL * (i >> 1) + ((i & 1) ? D::RL - 1 : 0) : 16 * t + i;
     const int k = dif_bin<N>(q);
     float mult;
     const int j = welch_slot(g, k, mult);
-    if (j >= 0) row[j] = 20.f * log10f(acc[i] * g.scale * mult);
+    if (j >= 0) row[j] = g.split > 1 ? acc[i] * g.scale * mult : 20.f * log10f(acc[i] * g.scale * mult);
+  }
+}
+
+// The split form's second launch: row j = 20 log10 of the parts' sum, in part order.
+__global__ void __launch_bounds__(256) welch_parts_kernel(const float *__restrict__ parts, WelchGeom g,
+                                                          float *__restrict__ rows) {
+  const int f = blockIdx.y;
+  const int n = g.onesided ? g.row_len : (g.n_win & ~1);
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    const float *pp = parts + (int64_t)f * g.split * g.n_win + j;
+    float sum = 0.f;
+    for (int q = 0; q < g.split; ++q) sum += pp[(int64_t)q * g.n_win];
+    rows[(int64_t)f * g.n_win + j] = 20.f * log10f(sum);
   }
 }
 
 #undef DIF_X
 #undef DIF_W
 
+constexpr int kDifMinSplit = 1024;
 template <int N>
 static hipError_t welch_dif_launch(const float2 *x, int64_t len, const float *win, const float2 *tw,
                                    const WelchGeom &g, float *rows, int frames, hipStream_t st) {
@@ -1008,14 +1026,32 @@ static hipError_t welch_dif_launch(const float2 *x, int64_t len, const float *wi
     if (e != hipSuccess) return e;
     attr_set[prune] = true;
   }
-  const dim3 grid((unsigned)((frames + D::FPB - 1) / D::FPB)), block(D::NT);
+  const dim3 grid((unsigned)((frames + D::FPB - 1) / D::FPB), (unsigned)g.split), block(D::NT);
   if (prune)
     hipLaunchKernelGGL((welch_dif_kernel<N, true>), grid, block, lds, st, (const v2f *)x, len, win,
                        (const v2f *)tw, g, rows, frames);
   else
     hipLaunchKernelGGL((welch_dif_kernel<N, false>), grid, block, lds, st, (const v2f *)x, len, win,
                        (const v2f *)tw, g, rows, frames);
+  if (g.split > 1) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int n = g.onesided ? g.row_len : (g.n_win & ~1);
+    hipLaunchKernelGGL(welch_parts_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)frames), dim3(256), 0,
+                       st, (const float *)g.parts, g, rows);
+  }
   return hipGetLastError();
+}
+
+int welch_dif_split(int n_fft, int nseg, int frames) {
+  if (n_fft < kDifMinSplit || n_fft > 16384 || nseg < 4) return 1;
+  const int fpb = n_fft / 16 >= 256 ? 1 : 256 / (n_fft / 16);
+  const int blocks = (frames + fpb - 1) / fpb;
+  const int target = 768 * 256 / std::max(256, n_fft / 16);  // workgroups that fill the chip
+  if (blocks >= target / 2) return 1;
+  const int want = std::min((target + blocks - 1) / blocks, nseg / 2);
+  const int per = (nseg + want - 1) / want;
+  return (nseg + per - 1) / per;  // every part non-empty
 }
 
 // ------------------------------------------------------------------ Welch row, four-step
@@ -1405,6 +1441,15 @@ hipError_t launch_fused_pass(const float2 *in, float2 *out, bool desc, bool two,
     hipLaunchKernelGGL((fused_pass_kernel<true, false, false>), dim3(blocks), dim3(256), 0, st, i, o, g, frames, c);
   else
     hipLaunchKernelGGL((fused_pass_kernel<false, false, false>), dim3(blocks), dim3(256), 0, st, i, o, g, frames, c);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void fill_c64_kernel(v2f *__restrict__ out, int64_t n, v2f v) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) out[k] = v;
+}
+hipError_t launch_fill_c64(float2 *out, int64_t n, float re, float im, hipStream_t st) {
+  hipLaunchKernelGGL(fill_c64_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, (v2f *)out, n, v2f{re, im});
   return hipGetLastError();
 }
 

@@ -405,7 +405,9 @@ struct zfft_plan {
   int welch = 0;  // 0 auto, 1 one workgroup per frame, 2 four-step
   DevBuf edge, xk, xa_tab, tws, means, z4, winf;
   DevBuf pc_tab, pc_edge;  // PC decimator: PcTab; edge maps U0 V0 U1 V1 (floats)
-  DevBuf pc_tab4;          // PC zoom 4: PcTab4
+  DevBuf pc_tab4;  // PC zoom 4: PcTab4
+  DevBuf wparts;   // split DIF Welch: partial PSDs (frames x split x n_win floats)
+  DevBuf lo1;      // unit LO table (the blocked passes after the PC head mix with it)
                            // (pc_edge: all nine maps of pc_edge_maps.h, uploaded once)
   int64_t n_quiesce = 0;   // host waits on enqueued work (test hook zfft__plan_quiesce_count)
   // waterfall rendering: colormap LUT (host copy + device), levels
@@ -586,18 +588,20 @@ int check_lengths(const zfft_plan *p, int64_t L, int32_t frames, std::vector<int
 // stage) in natural layout in *out.
 // With split > 0 (a multiple of 64) the frames [split, split + frames) are a second window
 // set starting alt_off samples into the same frames; the output then has split + frames rows.
+// k0 > 0: stages k0 .. K-1 only, `in` holding stage k0's input (already mixed: lo a unit
+// table), e.g. after the PC head.
 int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
               const std::vector<int64_t> &n, const float2 **out, hipStream_t st, int split = 0,
-              int64_t alt_off = 0) {
+              int64_t alt_off = 0, int k0 = 0) {
   const int rows = split > 0 ? split + frames : frames;
   const int ngroups = (rows + 63) / 64;
   const size_t G = (size_t)ngroups * 64;
-  hipError_t e = p->yf.ensure(G * (n[0] + 2 * kPad) * sizeof(float2));
-  if (e == hipSuccess) e = p->ping.ensure(G * n[1] * sizeof(float2));
-  if (e == hipSuccess && p->K > 1) e = p->pong.ensure(G * n[2] * sizeof(float2));
+  hipError_t e = p->yf.ensure(G * (n[k0] + 2 * kPad) * sizeof(float2));
+  if (e == hipSuccess) e = p->ping.ensure(G * n[k0 + 1] * sizeof(float2));
+  if (e == hipSuccess && p->K > k0 + 1) e = p->pong.ensure(G * n[k0 + 2] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   const float2 *cur = nullptr;
-  for (int k = 0; k < p->K; ++k) {
+  for (int k = k0; k < p->K; ++k) {
     StageGeom g;
     g.n = (int)n[k];
     g.block = choose_block(p, n[k], ngroups);
@@ -606,13 +610,13 @@ int run_exact(zfft_plan *p, const InDesc &in, const float2 *lo, int frames,
     g.ngroups = ngroups;
     g.split = split;
     g.alt_off = alt_off;
-    if (k == 0)
+    if (k == k0)
       e = launch_iir_forward_mix(in, frames, lo, p->yf.as<float2>(), g, st);
     else
       e = launch_iir_forward_fgi(cur, p->yf.as<float2>(), g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_forward launch");
     mark(p, st, k == 0 ? "exact_forward_mix" : "exact_forward");
-    float2 *dst = (k & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
+    float2 *dst = ((k - k0) & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
     e = launch_iir_backward(p->yf.as<float2>(), dst, k == p->K - 1, rows, g, st);
     if (e != hipSuccess) return hip_fail(e, "iir_backward launch");
     mark(p, st, "exact_backward");
@@ -892,13 +896,32 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
   return ZFFT_OK;
 }
 
-// PC head (3 stages into pong) + XA for stages 3 .. K-1 (ping, pong, ... in turn; no LO mix).
+// PC head (3 stages into pong), then stages 3 .. K-1 on its output (no LO mix): XA where XA
+// takes the batch (ping, pong, ... in turn), else the exact blocked passes (few frames per
+// call, the reference's one: a unit LO table stands for the mix their first pass applies).
 int run_pc_head(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vector<int64_t> &n,
                 bool walk, const float2 **out, hipStream_t st) {
   const float2 *cur = nullptr;
+  const int64_t n3 = n[kPcStages];
+  const bool xa_tail = auto_xa(frames, n3);
+  hipError_t e = hipSuccess;
+  if (!xa_tail) {  // pong must not move under the head's output when the blocked passes size it
+    const size_t G = (size_t)(frames + 63) / 64 * 64;
+    e = p->pong.ensure(std::max((size_t)frames * n3, p->K > kPcStages + 1 ? G * n[kPcStages + 2] : 0) *
+                       sizeof(float2));
+    if (e == hipSuccess && p->lo1.cap < (size_t)n3 * sizeof(float2)) {
+      e = p->lo1.ensure((size_t)n3 * sizeof(float2));
+      if (e == hipSuccess) e = launch_fill_c64(p->lo1.as<float2>(), n3, 1.f, 0.f, st);
+    }
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+  }
   int rc = run_pc(p, in, L, frames, n, walk, &cur, st, kPcStages);
   if (rc) return rc;
-  hipError_t e = p->ping.ensure((size_t)frames * n[kPcStages + 1] * sizeof(float2));
+  if (!xa_tail) {
+    const InDesc src{cur, n3, n3, kInC64, 0};
+    return run_exact(p, src, p->lo1.as<float2>(), frames, n, out, st, 0, 0, kPcStages);
+  }
+  e = p->ping.ensure((size_t)frames * n[kPcStages + 1] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   for (int k = kPcStages; k < p->K; ++k) {
     float2 *dst = ((k - kPcStages) & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
@@ -932,9 +955,8 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   // against 2.03 ms for XA) -- tools/sweep_schedule.py, profiles/r04l
   if (pc8 && (p->path == 0 || p->path == 4 || p->path == 5))
     return run_pc(p, in, L, frames, n, walk, out, st, p->K);
-  // zoom >= 16: the head where XA would take the batch (its tail stages are XA's)
-  if (p->path == 4 || p->path == 5 ||
-      (p->path == 0 && head && auto_xa(frames, n[kPcStages]) && xa_fits(p, L)))
+  // zoom >= 16: the head, then XA or the blocked passes for the rest (by the tail's batch)
+  if (p->path == 4 || p->path == 5 || (p->path == 0 && head && xa_fits(p, L)))
     return run_pc_head(p, in, L, frames, n, walk, out, st);
   if (p->path == 3 || (p->path == 0 && auto_xa(frames, L) && xa_fits(p, L)))
     return run_xa(p, in, frames, n, out, st);
@@ -1033,6 +1055,14 @@ int process_device(zfft_plan *p, const void *d_iq, int64_t L, int32_t frames, fl
     }
     mark(p, st, "welch4");
   } else {
+    // few frames per call (the reference's one): each frame's segments over several
+    // workgroups (welch_dif_split), partial PSDs summed by a second launch
+    if (nperseg == N) w.split = welch_dif_split(N, w.nseg, frames);
+    if (w.split > 1) {
+      e = p->wparts.ensure((size_t)frames * w.split * p->cfg.n_win * sizeof(float));
+      if (e != hipSuccess) return fail(ZFFT_ENOMEM, "Welch workspace allocation failed");
+      w.parts = p->wparts.as<float>();
+    }
     e = launch_welch_rows(x, Ld, p->win.as<float>(), p->tw.as<float2>(), w, d_rows, frames, st);
     if (e != hipSuccess) return hip_fail(e, "welch_rows launch");
     mark(p, st, "welch_rows");
@@ -1208,7 +1238,8 @@ int zfft_plan_destroy(zfft_plan *p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->in2, &p->yf, &p->ping, &p->pong, &p->rows,
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
-                    &p->tws, &p->means, &p->z4, &p->winf, &p->pc_tab, &p->pc_edge})
+                    &p->tws, &p->means, &p->z4, &p->winf, &p->pc_tab, &p->pc_edge, &p->pc_tab4,
+                    &p->wparts, &p->lo1, &p->lut_d, &p->rgba, &p->al_hist, &p->al_bins})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->done_ev) (void)hipEventDestroy(p->done_ev);

@@ -228,6 +228,23 @@ def test_welch_one_workgroup_forms_vs_oracle(oracle_lib, N, z, W, F):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, z, W), f"N={N} W={W} frame {f}")
 
 
+@pytest.mark.parametrize("N,z,W,L", [(4096, 2, 2048, 299008), (1024, 4, 256, 262144), (16384, 1, 16384, 294912),
+                                      (2048, 1, 2047, 100003), (8192, 8, 1024, 1048576), (4096, 1, 1000, 40960)])
+def test_welch_split_few_frames_vs_oracle(oracle_lib, N, z, W, L):
+    """A call of one or two frames -- the reference's use -- splits each frame's segments over
+    several workgroups (welch_dif_split) and sums their partial PSDs in a second launch:
+    rows within the gate (pruned and full last stage, odd W, zoom 1), identical on a repeat."""
+    from pypanadapter_amd import ZoomFFT
+    for F in (1, 2):
+        x = _frames(F, L, N, z, W, seed0=9300 + N + z + F)
+        with ZoomFFT(N, z, 2.4e6, n_win=W) as plan:
+            rows = plan.rows(x)
+            again = plan.rows(x)
+        np.testing.assert_array_equal(rows, again)
+        for f in range(F):
+            assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, z, W), f"N={N} z={z} F={F} frame {f}")
+
+
 @pytest.mark.parametrize("welch", [0, 1, 2])
 @pytest.mark.parametrize("N,z,W", [(16384, 1, 16384), (16384, 2, 8192), (16384, 1, 12000)])
 def test_welch_16384_unpruned_vs_oracle(oracle_lib, welch, N, z, W):
@@ -410,14 +427,14 @@ def test_facade_matches_reference_rows():
                                         (4, 1, 262144, "exact"), (4, 256, 262144, "exact"),
                                         (4, 384, 262144, "xa"), (4, 64, 1048576, "exact"),
                                         (4, 128, 1048576, "fused"), (4, 768, 1048576, "xa"),
-                                        (16, 384, 262144, "pc"), (16, 8, 262144, "exact")])
+                                        (16, 384, 262144, "pc"), (16, 8, 262144, "pc")])
 def test_auto_schedule_by_batch(z, F, L, want):
     """The automatic decimator schedule follows the measured crossovers (zfft_plan.cpp
     pc_fits / kPcWalkMinFrames / auto_xa / use_fused, tools/sweep_schedule.py,
     profiles/r04l): at zoom 8 the PC polyphase cascade for every batch of frames >= 16384
     samples (one frame per call -- the reference's use -- included), as its walk kernel
     from 4096 frames per call; zoom >= 16 as PC's first three stages + XA where XA would take
-    the batch; elsewhere small batches run the exact blocked passes,
+    the batch (the blocked passes on the 1/8-rate output below that); elsewhere small batches run the exact blocked passes,
     batches of >= 2^27 samples the fused interior with edge windows, and >= 384 frames of
     <= 2^19 samples (768 of longer ones) the XA tiles."""
     import torch
@@ -436,8 +453,8 @@ def test_auto_schedule_by_batch(z, F, L, want):
              "xa": ("xa_stage_mix",), "pc": ("pc_fir",), "walk": ("pc_walk",)}[want]
     assert names[0] in first, names
     assert ("edge_windows" in names) == (want == "fused"), names
-    if z == 16:  # the PC head's tail stage
-        assert ("xa_stage" in names) == (want == "pc"), names
+    if z == 16:  # the PC head's tail stage: XA's where XA takes the batch, else the blocked passes
+        assert ("xa_stage" in names) == (F >= 384) and ("exact_backward" in names) == (F < 384), names
     del x, rows
     torch.cuda.empty_cache()
 

@@ -226,8 +226,9 @@ def test_pc_ragged_lengths_on_a_caller_stream(oracle_lib, zfft_lib, path):
 @pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
 @PC_PATHS
 def test_pc_head_decimate_vs_oracle(oracle_lib, zoom, flip, path):
-    """decimate(x, 2) x log2(zoom) as PC's exact x8 (frame-end maps at every L mod 8) followed
-    by XA's stages on its output, against the float64 oracle; XA's 1e-5 per stage on top."""
+    """decimate(x, 2) x log2(zoom) as PC's exact x8 (frame-end maps at every L mod 8) followed,
+    for one frame per call, by the exact blocked passes on its output (a unit LO table), against
+    the float64 oracle; 1e-5 per tail stage on top."""
     from pypanadapter_amd import ZoomFFT
     rng = np.random.default_rng(4600 + zoom + flip)
     for L in [16384, 16387, 16390, 3968 * 5 + 1, 262144 + 5, 299008]:
@@ -238,7 +239,7 @@ def test_pc_head_decimate_vs_oracle(oracle_lib, zoom, flip, path):
             plan.set_timing(True)
             d = plan.decimate(x)
             names = plan.launch_names()
-        assert names.count("xa_stage") == {16: 1, 32: 2}[zoom], names
+        assert names.count("exact_backward") == {16: 1, 32: 2}[zoom], names  # one frame: blocked tail
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, zoom, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
         err = np.abs(d - ref) / np.abs(ref).max()
@@ -266,7 +267,7 @@ def test_pc_head_golden_rows(path):
 
 def test_pc_head_auto_batch_rows(oracle_lib):
     """At a batch XA would take (384 frames), zoom 16 runs the PC head + one XA stage on its
-    own; rows of three frames against the oracle."""
+    own (the XA tail); rows of three frames against the oracle."""
     from pypanadapter_amd import ZoomFFT
     F, L, N = 384, 65536 + 3, 2048
     x = np.zeros((F, L), np.complex64)
