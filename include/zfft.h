@@ -201,8 +201,8 @@ int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *coun
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
 /* Decimator schedule: 0 = automatic -- for zoom 8 and frames of >= 16384 samples 4 below
- * 4096 frames per call and 5 from there (zoom >= 16: the same as the first three stages when
- * the batch is XA's, below); otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
+ * 4096 frames per call and 5 from there (zoom >= 16: the same for the first three stages;
+ * zoom 4: 4 below 1024 frames per call); otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
  * samples, else 2 for batches of >= 2^27 samples whose frames are long enough for the edge
  * windows, else 1 -- e.g. one frame per call, the reference's use.  Each batch of a
  * zfft_process call is judged by its own frame count (host calls are split into batches of
@@ -221,7 +221,8 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * same arithmetic as one launch with one workgroup per frame (the rate-1/4 intermediate
  * stays on chip; automatic from 4096 frames per call); at zoom 4, path 5 is the two-stage
  * form of the walk (FIR, own-rate sections at rate 1/2, 41-tap FIR, 6 output-rate sections;
- * on request only: XA is faster there); at zoom >= 16, paths 4 / 5 run PC (tiles / walk) for the
+ * on request only: XA is faster there) and path 4 its tiles (automatic below 1024 frames per
+ * call, XA from there); at zoom >= 16, paths 4 / 5 run PC (tiles / walk) for the
  * first three stages and XA for the rest on its 1/8-rate output -- the automatic choice
  * wherever XA would take the batch (zoom 16 on cfg2's frames: 5.23 against XA's 6.35 ms per
  * 4096 frames).  Path 3

@@ -229,15 +229,20 @@ __device__ __forceinline__ void load_pair(const InDesc &in, int64_t f, int64_t n
 // x[4 q_s - 64, + 4128) (zero outside the frame):
 //   y1[m] = sum_t g0[t + 16] x[2m - t],  m in [2 q_s - 24, + 2048)   (8 per thread)
 //   y2[q] = sum_t g1[t + 24] y1[2q - t]                            (4 per thread)
-template <int DT, int FLIP>
+template <int ZOOM> struct PcTabOf { typedef CT T; };
+template <> struct PcTabOf<4> { typedef CT4 T; };
+// ZOOM = 4: FIR alpha only, y1 [m_s, m_s + 2048), m_s = kPc4Q0 + 2048 tile, from the mixed
+// input x[2 m_s - 16, + 4128) -- the same input tile and thread map -- written to y2 (= y1 here)
+template <int DT, int FLIP, int ZOOM>
 __global__ void __launch_bounds__(256) pc_fir_kernel(InDesc in, const v2f *lo, v2f *y2,
-                                                     int64_t y2s, CT tab) {
+                                                     int64_t y2s, typename PcTabOf<ZOOM>::T tab) {
   __shared__ v4f lds4[kXRows * kXRow / 2];
   const LP xl = (LP)lds4;
   const int t = threadIdx.x;
   const int tile = blockIdx.x;
   const int64_t f = blockIdx.y, L = in.len;
-  const int64_t xs = 4 * ((int64_t)kPcQ0 + (int64_t)kPcK1Q * tile) - 64;
+  const int64_t xs = ZOOM == 4 ? 2 * ((int64_t)kPc4Q0 + (int64_t)kPc4K1M * tile) - 16
+                               : 4 * ((int64_t)kPcQ0 + (int64_t)kPcK1Q * tile) - 64;
   const v2f *lor = lo_row(lo, in, f);
   if (xs >= 0 && xs + kPcK1In <= L) {
     // LO factor lo[n0 + 2t + j] = lo[n0] lo[2t + j] / sqrt 2 (the table is an exact
@@ -287,12 +292,18 @@ __global__ void __launch_bounds__(256) pc_fir_kernel(InDesc in, const v2f *lo, v
       }
     }
   }
+  if constexpr (ZOOM == 4) {
+    v2f *o = y2 + f * y2s + (int64_t)kPc4K1M * tile + 8 * t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(v4f *)(o + 2 * q) = cat(acc[2 * q], acc[2 * q + 1]);
+    return;
+  }
   __syncthreads();
   const LP yl = xl;
 #pragma unroll
   for (int q = 0; q < 4; ++q) *(LP4)(yl + t * kYRow + 2 * q) = cat(acc[2 * q], acc[2 * q + 1]);
   __syncthreads();
-  if (t < kPcK1Q / 4) {
+  if constexpr (ZOOM == 8) if (t < kPcK1Q / 4) {
     v2f b[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) b[r] = splat(0.f);
@@ -352,9 +363,9 @@ __device__ __forceinline__ void walk_prio(bool recurrence) {
 // response ct[t] for t < DCUT.  XW: the block's 4 waves continue each other (one
 // cross-wave step through scr: 4 waves x 2 states); otherwise lane 0 (UP) / 63 enters
 // from a zero state.
-template <int B, int LEV, int DCUT, bool UP, bool XW, bool OWN, int SI>
-__device__ __forceinline__ void sec_block(v2f (&v)[B], CT tab0, LP scr, int lane, int wave) {
-  const CT tab = fresh(tab0);
+template <int B, int LEV, int DCUT, bool UP, bool XW, bool OWN, int SI, class TP>
+__device__ __forceinline__ void sec_block(v2f (&v)[B], TP tab0, LP scr, int lane, int wave) {
+  const TP tab = fresh(tab0);
   CS S = OWN ? tab->own[SI] : tab->ap[SI];
   const v2f na1 = splat(-S.a1), na2 = splat(-S.a2);
   v2f y1 = splat(0.f), y2 = splat(0.f);
@@ -462,15 +473,17 @@ static_assert(kApWave == kPcK2M / 4 + 2 * kPcApHalo, "one wave per quarter tile 
 static_assert(kU3Base - kPcApHalo + 3 * (kPcK2M / 4) + kApWave <= kU3, "u3 covers the waves");
 
 // One tile: outputs [m0, m0 + 2048), m0 = 2048 tile, from y2 over [2 m0 - 560, + 5376).
+// ZOOM = 4: the same on y1 (stored from kPc4Q0) with zoom 4's FIR g1 and output-rate sections.
+template <int ZOOM>
 __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s, int64_t y2n,
-                                                      v2f *out, int64_t n3, CT tab) {
+                                                      v2f *out, int64_t n3, typename PcTabOf<ZOOM>::T tab) {
   __shared__ v4f sp4[kPcK2Span / 2];
   __shared__ v4f scr4[4 * 4];
   const LP sp = (LP)sp4;
   const LP scr = (LP)scr4;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t f = blockIdx.y, m0 = (int64_t)kPcK2M * blockIdx.x;
-  const int64_t g0 = 2 * m0 - kPcK2Left - kPcQ0;  // y2 entry of span sample 0
+  const int64_t g0 = 2 * m0 - kPcK2Left - (ZOOM == 4 ? kPc4Q0 : kPcQ0);  // y2 entry of span sample 0
   const v2f *yb = y2 + f * y2s;
   for (int s = 2 * t; s < kPcK2Span; s += 512) {
     const int64_t g = g0 + s;  // even: a pair is wholly inside or outside [0, y2n)
@@ -501,18 +514,20 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
 #pragma unroll
     for (int r = 0; r < 9; ++r) u[r] = sp[18 * t + 2 * r + 304];
   } else {
-    const LP zb = sp + 18 * t + (kPcK2Left - 2 * kU3Base) - (kPcG2 - 1) / 2;
+    // zoom 8: g2 (57 taps) on z2; zoom 4: g1 (41 taps) on z1
+    constexpr int G = ZOOM == 4 ? kPc4G1 : kPcG2;
+    const auto taps = [&]() {
+      if constexpr (ZOOM == 8) return tab->g2;
+      else return tab->g1;
+    };
+    const LP zb = sp + 18 * t + (kPcK2Left - 2 * kU3Base) - (G - 1) / 2;
 #pragma unroll
-    for (int p = 0; p < 37; ++p) {
+    for (int p = 0; p < (G + 17) / 2; ++p) {
       const int j = 2 * p;
       const v4f w = *(LP4)(zb + j);
       const v2f x0 = lo2(w), x1 = hi2(w);
 #pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        const int q = j - 2 * r;
-        if (q >= 0 && q < kPcG2) u[r] = vfma(splat(tab->g2[q]), x0, u[r]);
-        if (q + 1 >= 0 && q + 1 < kPcG2) u[r] = vfma(splat(tab->g2[q + 1]), x1, u[r]);
-      }
+      for (int r = 0; r < 9; ++r) fir_pair<G>(u[r], taps(), j - 2 * r, x0, x1);
     }
   }
   __syncthreads();
@@ -986,16 +1001,32 @@ hipError_t launch_pc_fir(const InDesc &in, const float2 *lo, float2 *y2, int64_t
   const int ntiles = (int)((pc_y2_len(in.len) + kPcK1Q - 1) / kPcK1Q);
   const dim3 grid(ntiles, frames);
   const pc::CT ct = (pc::CT)tab;
-  PC_DISPATCH(pc::pc_fir_kernel, in, grid, dim3(256), 0, st, in, (const v2f *)lo, (v2f *)y2,
-              y2_stride, ct);
+  PC_DISPATCH_Z(pc::pc_fir_kernel, 8, in, grid, dim3(256), 0, st, in, (const v2f *)lo, (v2f *)y2,
+                y2_stride, ct);
   return hipGetLastError();
 }
 
 hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int64_t n3,
                           int frames, const PcTab *tab, hipStream_t st) {
   const dim3 grid((unsigned)((n3 + kPcK2M - 1) / kPcK2M), frames);
-  hipLaunchKernelGGL(pc::pc_tail_kernel, grid, dim3(256), 0, st, (const v2f *)y2, y2_stride,
+  hipLaunchKernelGGL(pc::pc_tail_kernel<8>, grid, dim3(256), 0, st, (const v2f *)y2, y2_stride,
                      y2_stride, (v2f *)out, n3, (pc::CT)tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_pc4_fir(const InDesc &in, const float2 *lo, float2 *y1, int64_t y1_stride,
+                          int frames, const PcTab4 *tab, hipStream_t st) {
+  const dim3 grid((unsigned)((pc4_y1_len(in.len) + kPc4K1M - 1) / kPc4K1M), frames);
+  PC_DISPATCH_Z(pc::pc_fir_kernel, 4, in, grid, dim3(256), 0, st, in, (const v2f *)lo, (v2f *)y1,
+                y1_stride, (pc::CT4)tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_pc4_tail(const float2 *y1, int64_t y1_stride, int64_t y1n, float2 *out, int64_t n2,
+                           int frames, const PcTab4 *tab, hipStream_t st) {
+  const dim3 grid((unsigned)((n2 + kPcK2M - 1) / kPcK2M), frames);
+  hipLaunchKernelGGL(pc::pc_tail_kernel<4>, grid, dim3(256), 0, st, (const v2f *)y1, y1_stride, y1n,
+                     (v2f *)out, n2, (pc::CT4)tab);
   return hipGetLastError();
 }
 

@@ -277,6 +277,8 @@ int64_t pc_y2_len(int64_t L) {
   return (m_hi + 24) / 2 + 1 - kPcQ0;
 }
 
+int64_t pc4_y1_len(int64_t L) { return (L + 15) / 2 + 1 - kPc4Q0; }
+
 bool pc_build_tables(PcTab &tab) {
   std::memset(&tab, 0, sizeof(tab));
   const Lev &l = levels();
@@ -338,6 +340,8 @@ bool pc_build_tables4(PcTab4 &tab) {
   std::memcpy(tab.wb, t8.wb, sizeof(tab.wb));
   std::memcpy(tab.wf_x, t8.wf_x, sizeof(tab.wf_x));
   std::memcpy(tab.wb_x, t8.wb_x, sizeof(tab.wb_x));
+  std::memcpy(tab.own, t8.own, sizeof(tab.own));
+  std::memcpy(tab.own_x, t8.own_x, sizeof(tab.own_x));
   // output-rate sections: D4 (stage 0 moved twice), D2 sections 0, 1 (stage 1), slowest first
   std::vector<std::pair<double, double>> ap;
   for (int k = 0; k < 4; ++k) ap.emplace_back(l.d[2].a1[k], l.d[2].a2[k]);

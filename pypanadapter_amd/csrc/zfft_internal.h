@@ -199,7 +199,19 @@ struct PcTab4 {
   PcSec ap[kPc4Ap];                 // B = 11, slowest first
   PcSec wf[kPcOwn], wb[kPcOwn];     // own-rate sections (those of PcTab)
   float wf_x[kPcOwn][64][4], wb_x[kPcOwn][64][4];
+  PcSec own[kPcOwn];                // the tiles' own-rate sections (B = 21, those of PcTab)
+  float own_x[kPcOwn][64][4];
 };
+// Zoom 4 as tiles (path 4; few frames per call): K1 = FIR alpha only, y1 (the own-rate signal)
+// through device memory from index kPc4Q0 in tiles of 2048; K2 = zoom 8's tail kernel on y1
+// with zoom 4's FIR g1 and 6 output-rate sections.
+constexpr int kPc4Q0 = -8;               // first y1 index of the model's support
+constexpr int kPc4K1M = 2048;            // y1 per K1 tile
+int64_t pc4_y1_len(int64_t L);           // y1 entries per frame (from kPc4Q0)
+hipError_t launch_pc4_fir(const InDesc &in, const float2 *lo, float2 *y1, int64_t y1_stride,
+                          int frames, const PcTab4 *tab, hipStream_t st);
+hipError_t launch_pc4_tail(const float2 *y1, int64_t y1_stride, int64_t y1n, float2 *out, int64_t n2,
+                           int frames, const PcTab4 *tab, hipStream_t st);
 __host__ __device__ constexpr int pc4_ap_levels(int s) { return s == 0 ? 3 : s <= 2 ? 2 : s <= 4 ? 1 : 0; }
 __host__ __device__ constexpr int pc4_ap_dcut(int) { return kPcApBlk; }
 bool pc_build_tables4(PcTab4 &tab);

@@ -793,13 +793,19 @@ constexpr int kPcWalkMinFrames = 4096;
 bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == kPcStages && L >= kPcMinL && frames <= 65535;
 }
-// Zoom 4 (two stages) has the walk form only (pc_walk_kernel<4>), on request (path 5): at cfg1
-// (F = 4096, L = 262,144) it takes 4.49-4.50 ms against XA's 2.89 + 1.45 = 4.34 ms on the same
-// box (profiles/r05h) -- at zoom 4 the recurrences run on twice the share of the samples they
-// see at zoom 8, and they are the walk's latency-bound half -- so the automatic choice stays XA.
+// Zoom 4 (two stages): the walk (pc_walk_kernel<4>, path 5, on request: at cfg1 -- F = 4096,
+// L = 262,144 -- it takes 4.49-4.50 ms against XA's 2.89 + 1.45 = 4.34 ms on the same box,
+// profiles/r05h: at zoom 4 the recurrences run on twice the share of the samples they see at
+// zoom 8, and they are the walk's latency-bound half) and the tiles (K1 = FIR alpha into y1,
+// K2 = the zoom-8 tail kernel on zoom 4's tables: path 4, and automatic below XA's batch).
 bool pc4_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == 2 && L >= kPcMinL && frames <= 65535;
 }
+// Zoom-4 tiles against XA (cfg1's 262,144-sample frames, profiles/r05u, ms per call): 1 frame
+// 0.061 / 1.14 (blocked passes 0.22), 64: 0.14 / 1.21 (0.28), 256: 0.46 / 1.24, 384: 0.65 /
+// 1.26, 1024: 1.64 / 1.56 -- XA, one wave per frame, needs about a thousand frames to fill the
+// chip.
+constexpr int kPc4TilesMaxFrames = 1024;
 // Zoom >= 16: PC takes the first three stages (decimate x 3 exactly, frame-end maps included)
 // and XA the remaining K - 3 on its 1/8-rate output -- the reference's stages are applied one
 // after another (S:2096-2098), so the composition is the same cascade.
@@ -858,7 +864,19 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
   const int64_t n3 = n[K];
   const PcTab *tab = p->pc_tab.as<PcTab>();
   hipError_t e;
-  if (K == 2) {  // zoom 4: the walk only
+  if (K == 2 && !walk) {  // zoom 4 as tiles: K1 (FIR alpha) -> y1 (ping) -> K2 -> out (pong)
+    const int64_t y1s = (pc4_y1_len(L) + kPc4K1M - 1) / kPc4K1M * kPc4K1M;
+    e = p->ping.ensure((size_t)frames * y1s * sizeof(float2));
+    if (e == hipSuccess) e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+    e = launch_pc4_fir(in, p->lo.as<float2>(), p->ping.as<float2>(), y1s, frames, p->pc_tab4.as<PcTab4>(), st);
+    if (e != hipSuccess) return hip_fail(e, "pc_fir launch");
+    mark(p, st, "pc_fir");
+    e = launch_pc4_tail(p->ping.as<float2>(), y1s, y1s, p->pong.as<float2>(), n3, frames,
+                        p->pc_tab4.as<PcTab4>(), st);
+    if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
+    mark(p, st, "pc_tail");
+  } else if (K == 2) {  // zoom 4: the walk
     e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
     e = launch_pc_walk4(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab4.as<PcTab4>(), st);
@@ -944,11 +962,13 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  const bool pc8 = pc_fits(p, L, frames), head = pc_head_fits(p, L, frames);
-  if ((p->path == 4 && !pc8 && !head) || (p->path == 5 && !pc8 && !head && !pc4_fits(p, L, frames)))
-    return fail(ZFFT_EUNSUPPORTED, "PC decimator needs zoom >= 8 (path 4, 5) or zoom 4 (path 5), "
-                                   "frames of >= 16384 samples and <= 65535 frames per call");
-  if (p->path == 5 && pc4_fits(p, L, frames)) return run_pc(p, in, L, frames, n, true, out, st, p->K);
+  const bool pc8 = pc_fits(p, L, frames), head = pc_head_fits(p, L, frames), pc4 = pc4_fits(p, L, frames);
+  if ((p->path == 4 || p->path == 5) && !pc8 && !head && !pc4)
+    return fail(ZFFT_EUNSUPPORTED, "PC decimator needs zoom >= 4 (paths 4, 5), frames of >= 16384 "
+                                   "samples and <= 65535 frames per call");
+  // zoom 4: the walk on request, the tiles on request and automatic below 1024 frames per call
+  if (pc4 && (p->path == 4 || p->path == 5 || (p->path == 0 && frames < kPc4TilesMaxFrames)))
+    return run_pc(p, in, L, frames, n, p->path == 5, out, st, p->K);
   const bool walk = p->path == 5 || (p->path == 0 && frames >= kPcWalkMinFrames);
   // PC is the fastest schedule wherever it applies, from one frame per call (the
   // reference's use: 0.083 against 0.37 ms for path 1) to full batches (1024 frames: 1.44
@@ -1381,7 +1401,8 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
     int nb = std::max<int64_t>(2, (int64_t)((total + kPipeBatchBytes - 1) / kPipeBatchBytes));
     B = (frames + nb - 1) / nb;
     const int need = L <= kXaShortFrame ? kXaMinFramesShort : kXaMinFrames;
-    if (p->path == 0 && p->K > 0 && !pc_fits(p, L, frames) && auto_xa(frames, L) && B < need) {
+    if (p->path == 0 && p->K > 0 && !pc_fits(p, L, frames) &&
+        !(pc4_fits(p, L, frames) && frames < kPc4TilesMaxFrames) && auto_xa(frames, L) && B < need) {
       nb = std::max(1, frames / need);
       B = (frames + nb - 1) / nb;
     }

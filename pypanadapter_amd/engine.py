@@ -121,7 +121,8 @@ class ZoomFFT:
         frame; auto for >= 768 frames, or >= 384 frames of <= 2^19 samples), 4 PC polyphase
         cascade tiles (zoom 8, frames >= 16384 samples; the auto choice there below 4096
         frames per call), 5 the PC walk (one workgroup per frame; zoom 8: auto from 4096
-        frames; zoom 4: the two-stage walk, on request only -- XA is faster there).  At zoom
+        frames; zoom 4: the two-stage walk, on request only -- XA is faster there; path 4 at
+        zoom 4 is its tiles, automatic below 1024 frames per call).  At zoom
         >= 16, 4 / 5 run PC for the first three stages and XA for the rest; automatic wherever
         XA would take the batch."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")

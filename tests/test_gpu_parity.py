@@ -424,9 +424,10 @@ def test_facade_matches_reference_rows():
 @pytest.mark.parametrize("z,F,L,want", [(8, 1, 299008, "pc"), (8, 384, 299008, "pc"),
                                         (8, 768, 1048576, "pc"), (8, 4096, 32768, "walk"),
                                         (8, 4095, 32768, "pc"), (8, 4, 8192, "exact"),
-                                        (4, 1, 262144, "exact"), (4, 256, 262144, "exact"),
-                                        (4, 384, 262144, "xa"), (4, 64, 1048576, "exact"),
-                                        (4, 128, 1048576, "fused"), (4, 768, 1048576, "xa"),
+                                        (4, 1, 262144, "pc"), (4, 256, 262144, "pc"),
+                                        (4, 384, 262144, "pc"), (4, 64, 1048576, "pc"),
+                                        (4, 1023, 65536, "pc"), (4, 1024, 65536, "xa"),
+                                        (2, 384, 262144, "xa"), (2, 8, 262144, "exact"),
                                         (16, 384, 262144, "pc"), (16, 8, 262144, "pc")])
 def test_auto_schedule_by_batch(z, F, L, want):
     """The automatic decimator schedule follows the measured crossovers (zfft_plan.cpp
@@ -434,15 +435,17 @@ def test_auto_schedule_by_batch(z, F, L, want):
     profiles/r04l): at zoom 8 the PC polyphase cascade for every batch of frames >= 16384
     samples (one frame per call -- the reference's use -- included), as its walk kernel
     from 4096 frames per call; zoom >= 16 as PC's first three stages + XA where XA would take
-    the batch (the blocked passes on the 1/8-rate output below that); elsewhere small batches run the exact blocked passes,
-    batches of >= 2^27 samples the fused interior with edge windows, and >= 384 frames of
-    <= 2^19 samples (768 of longer ones) the XA tiles."""
+    the batch (the blocked passes on the 1/8-rate output below that); at zoom 4 PC's zoom-4
+    tiles below 1024 frames per call and XA from there; elsewhere (zoom 2, frames < 16384
+    samples) >= 384 frames of <= 2^19 samples (768 of longer ones) the XA tiles and smaller
+    batches the exact blocked passes (the fused interior with edge windows is reached on
+    request only)."""
     import torch
     from pypanadapter_amd import ZoomFFT
     dev = torch.device("cuda", 0)
     x = torch.zeros((F, L, 2), dtype=torch.float32, device=dev)
     x[..., 0] = 1.0
-    N = {4: 1024, 8: 4096, 16: 4096}[z]
+    N = {2: 2048, 4: 1024, 8: 4096, 16: 4096}[z]
     rows = torch.empty((F, N // z), dtype=torch.float32, device=dev)
     with ZoomFFT(N, z, 2.4e6, n_win=N // z) as plan:
         plan.set_timing(True)
@@ -518,13 +521,14 @@ def test_xa_refuses_frames_beyond_32bit_offsets():
                                 torch.cuda.current_stream().cuda_stream)
 
 
-@pytest.mark.parametrize("z,F,L,first", [(8, 1024, 32768, "pc_fir"), (4, 1000, 32768, "xa_stage_mix"),
-                                          (4, 500, 32768, "xa_stage_mix")])
-def test_batched_host_call_times_every_batch_with_one_schedule(z, F, L, first):
+@pytest.mark.parametrize("z,F,L,first,waits", [(8, 1024, 32768, "pc_fir", 1), (4, 2100, 32768, "xa_stage_mix", 1),
+                                                (2, 1000, 32768, "xa_stage_mix", 1),
+                                                (2, 500, 32768, "xa_stage_mix", 0), (4, 500, 32768, "pc_fir", 1)])
+def test_batched_host_call_times_every_batch_with_one_schedule(z, F, L, first, waits):
     """zfft_process splits a >= 64 MB call into batches (H2D of k+1 under compute of k): the
     timings cover every batch, and a call the XA tiles would take keeps them in every batch
     (batches of >= 384 frames for these lengths, or a single batch) instead of splitting into
-    batches too small for them."""
+    batches too small for them; PC's tiles (zoom 8, zoom 4 below 1024 frames) take any batch."""
     from pypanadapter_amd import ZoomFFT
     x = np.zeros((F, L), np.complex64)
     x[:, ::3] = 1.0
@@ -534,7 +538,7 @@ def test_batched_host_call_times_every_batch_with_one_schedule(z, F, L, first):
         names = plan.launch_names()
     assert np.all(np.isfinite(rows))
     assert names.count(first) == names.count("batch_wait") + 1, names
-    assert names.count("batch_wait") == (0 if F < 768 else 1), names
+    assert names.count("batch_wait") == waits, names
 
 
 IF_LOS = [1.0 + k * 150e3 for k in range(8)]  # config 4's IF centre frequencies

@@ -156,7 +156,7 @@ def test_pc_matches_xa_and_exact_rows(oracle_lib):
 def test_pc_refuses_outside_its_domain(path):
     from pypanadapter_amd import ZoomFFT
     x = np.zeros(299008, np.complex64)
-    for zoom in ((2, 4) if path == 4 else (2,)):  # zoom 4 has the walk (path 5) only
+    for zoom in (2,):  # zoom 2 has no PC form
         with ZoomFFT(4096, zoom, 2.4e6) as plan:
             plan.set_path(path)
             with pytest.raises(NotImplementedError):
@@ -282,13 +282,14 @@ def test_pc_head_auto_batch_rows(oracle_lib):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, 16, 128), f"frame {f}")
 
 
-# ---- zoom 4: the walk (pc_walk_kernel<4>, path 5; automatic from 2048 frames) ----
+# ---- zoom 4: the tiles (path 4; automatic below XA's batch) and the walk (path 5) ----
 
 PC4_LENGTHS = [16384, 16385, 16386, 16387, 2048 * 9 + 3, 262144, 262144 + 2, 299008 + 1]
 
 
 @pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
-def test_pc4_decimate_vs_oracle(oracle_lib, flip):
+@PC_PATHS
+def test_pc4_decimate_vs_oracle(oracle_lib, flip, path):
     """Zoom 4's two-stage cascade (cfg1's decimator, S:2096-2098 at fft_ratio 4) at every
     L mod 4, against the float64 oracle of decimate(x, 2) twice."""
     from pypanadapter_amd import ZoomFFT
@@ -297,7 +298,7 @@ def test_pc4_decimate_vs_oracle(oracle_lib, flip):
         x = (rng.standard_normal(L) + 1j * rng.standard_normal(L)).astype(np.complex64)
         x += np.exp(2j * np.pi * 0.013 * np.arange(L)).astype(np.complex64)
         with ZoomFFT(1024, 4, 2.4e6, flip=flip) as plan:
-            plan.set_path(5)
+            plan.set_path(path)
             d = plan.decimate(x)
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 4, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
@@ -306,19 +307,21 @@ def test_pc4_decimate_vs_oracle(oracle_lib, flip):
 
 
 @pytest.mark.parametrize("N,L,F", [(1024, 262144, 5), (4096, 299008, 3), (2048, 131072 + 3, 4)])
-def test_pc4_rows_vs_oracle(oracle_lib, N, L, F):
+@PC_PATHS
+def test_pc4_rows_vs_oracle(oracle_lib, N, L, F, path):
     from pypanadapter_amd import ZoomFFT
     W = N // 4
     x = _frames(F, L, N, 4, W, seed0=8100 + N // 1024)
     with ZoomFFT(N, 4, 2.4e6, n_win=W) as plan:
-        plan.set_path(5)
+        plan.set_path(path)
         rows = plan.rows(x)
     for f in range(F):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, 4, W), f"N={N} L={L} frame {f}")
 
 
-def test_pc4_golden_rows():
-    """Every zoom-4 golden row the reference recorded whose frame the PC walk takes."""
+@PC_PATHS
+def test_pc4_golden_rows(path):
+    """Every zoom-4 golden row the reference recorded whose frame PC takes (tiles and walk)."""
     from pypanadapter_amd import ZoomFFT
     from conftest import window_of
     n = 0
@@ -328,7 +331,7 @@ def test_pc4_golden_rows():
         x = case_input(c)
         with ZoomFFT(c["n_fft"], 4, c["fs"], n_win=c["n_win"], window=window_of(c["window"]),
                      f_lo=c["f_lo"]) as plan:
-            plan.set_path(5)
+            plan.set_path(path)
             row = plan.rows(x)
         assert_row_close(row, golden_rows()[c["name"]], c["name"])
         n += 1
@@ -336,15 +339,16 @@ def test_pc4_golden_rows():
 
 
 @pytest.mark.parametrize("fmt", ["complex32", "cu8", "f32"])
-def test_pc4_input_formats_and_lo(oracle_lib, fmt):
-    """Raw-source formats, np.flip and per-frame LOs through the zoom-4 walk."""
+@PC_PATHS
+def test_pc4_input_formats_and_lo(oracle_lib, fmt, path):
+    """Raw-source formats, np.flip and per-frame LOs through zoom 4's tiles and walk."""
     from pypanadapter_amd import ZoomFFT
     F, L, N = 3, 262144 + 1, 1024
     f_lo = [1.0, 150e3 + 1.0, -300e3 + 1.0]
     x = np.stack([_frames(1, L, N, 4, 256, seed0=8300 + f, f_lo=f_lo[f])[0] for f in range(F)])
     arr, vals = _encode(x, fmt)
     with ZoomFFT(N, 4, 2.4e6, n_win=256, in_dtype=fmt, flip=True) as plan:
-        plan.set_path(5)
+        plan.set_path(path)
         plan.set_lo_frames(f_lo, 1)
         rows = plan.rows(arr)
     for f in range(F):
@@ -352,13 +356,14 @@ def test_pc4_input_formats_and_lo(oracle_lib, fmt):
                          f"{fmt} frame {f}")
 
 
-def test_pc4_size_independent_properties():
-    """Determinism, frame-order equivariance, exact x2 scaling, and the walk against the XA
-    schedule on the same batch."""
+@PC_PATHS
+def test_pc4_size_independent_properties(path):
+    """Determinism, frame-order equivariance, exact x2 scaling, and PC against the XA schedule
+    on the same batch."""
     from pypanadapter_amd import ZoomFFT
     x = _frames(8, 262144, 1024, 4, 256, seed0=8500)
     with ZoomFFT(1024, 4, 2.4e6) as plan:
-        plan.set_path(5)
+        plan.set_path(path)
         a = plan.rows(x)
         b = plan.rows(x)
         perm = np.random.default_rng(2).permutation(8)
