@@ -93,7 +93,6 @@ typedef v2f __attribute__((address_space(3))) *LP;
 typedef v4f __attribute__((address_space(3))) *LP4;
 typedef const PcTab __attribute__((address_space(4))) *CT;
 typedef const PcTab4 __attribute__((address_space(4))) *CT4;
-typedef const PcTab2 __attribute__((address_space(4))) *CT2;
 typedef const PcSec __attribute__((address_space(4))) &CS;
 
 __device__ __forceinline__ v2f shup(v2f v, int d) {
@@ -232,7 +231,6 @@ __device__ __forceinline__ void load_pair(const InDesc &in, int64_t f, int64_t n
 //   y2[q] = sum_t g1[t + 24] y1[2q - t]                            (4 per thread)
 template <int ZOOM> struct PcTabOf { typedef CT T; };
 template <> struct PcTabOf<4> { typedef CT4 T; };
-template <> struct PcTabOf<2> { typedef CT2 T; };
 // ZOOM = 4: FIR alpha only, y1 [m_s, m_s + 2048), m_s = kPc4Q0 + 2048 tile, from the mixed
 // input x[2 m_s - 16, + 4128) -- the same input tile and thread map -- written to y2 (= y1 here)
 template <int DT, int FLIP, int ZOOM>
@@ -465,13 +463,6 @@ __device__ __forceinline__ void ap_cascade(v2f (&a)[kPcApBlk], CT4 tab0, int lan
   sec_run<kPcApBlk, pc4_ap_levels(S), pc4_ap_dcut(S), UP>(a, tab->ap[S], lane);
   if constexpr (S + 1 < kPc4Ap) ap_cascade<S + 1, UP>(a, tab, lane);
 }
-// zoom 2's (PcTab2::ap, 2 sections)
-template <int S, bool UP>
-__device__ __forceinline__ void ap_cascade(v2f (&a)[kPcApBlk], CT2 tab0, int lane) {
-  const CT2 tab = fresh(tab0);
-  sec_run<kPcApBlk, pc2_ap_levels(S), pc2_ap_dcut(S), UP>(a, tab->ap[S], lane);
-  if constexpr (S + 1 < kPc2Ap) ap_cascade<S + 1, UP>(a, tab, lane);
-}
 
 constexpr int kU3 = 256 * 9;                   // FIR gamma outputs per tile (9 per thread)
 constexpr int kU3Base = 128;                    // u3 index k <-> output m0 - 128 + k
@@ -483,43 +474,22 @@ static_assert(kU3Base - kPcApHalo + 3 * (kPcK2M / 4) + kApWave <= kU3, "u3 cover
 
 // One tile: outputs [m0, m0 + 2048), m0 = 2048 tile, from y2 over [2 m0 - 560, + 5376).
 // ZOOM = 4: the same on y1 (stored from kPc4Q0) with zoom 4's FIR g1 and output-rate sections.
-// ZOOM = 2: the own-rate signal is the mixed input itself (span sample s = input sample
-// 2 m0 - 560 + s, zero outside the frame), zoom 2's 25-tap FIR and 2 output-rate sections.
-template <int ZOOM, int DT = kInC64, int FLIP = 0>
+template <int ZOOM>
 __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s, int64_t y2n,
-                                                      v2f *out, int64_t n3, typename PcTabOf<ZOOM>::T tab,
-                                                      InDesc in, const v2f *lo) {
+                                                      v2f *out, int64_t n3, typename PcTabOf<ZOOM>::T tab) {
   __shared__ v4f sp4[kPcK2Span / 2];
   __shared__ v4f scr4[4 * 4];
   const LP sp = (LP)sp4;
   const LP scr = (LP)scr4;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t f = blockIdx.y, m0 = (int64_t)kPcK2M * blockIdx.x;
-  if constexpr (ZOOM == 2) {
-    const int64_t n0 = 2 * m0 - kPcK2Left, L = in.len;
-    const v2f *lor = lo_row(lo, in, f);
-    for (int s = 2 * t; s < kPcK2Span; s += 512) {
-      const int64_t n = n0 + s;
-      v2f a = splat(0.f), b = splat(0.f);
-      if (n >= 0 && n + 2 <= L) {
-        load_pair<DT, FLIP>(in, f, n, a, b);
-        a = cmul2(a, lor[n]);
-        b = cmul2(b, lor[n + 1]);
-      } else {
-        if (n >= 0 && n < L) a = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
-        if (n + 1 >= 0 && n + 1 < L) b = cmul2(load_in_t<DT, FLIP>(in, f, n + 1), lor[n + 1]);
-      }
-      *(LP4)(sp + s) = cat(a, b);
-    }
-  } else {
-    const int64_t g0 = 2 * m0 - kPcK2Left - (ZOOM == 4 ? kPc4Q0 : kPcQ0);  // y2 entry of span sample 0
-    const v2f *yb = y2 + f * y2s;
-    for (int s = 2 * t; s < kPcK2Span; s += 512) {
-      const int64_t g = g0 + s;  // even: a pair is wholly inside or outside [0, y2n)
-      v4f w = v4f{0.f, 0.f, 0.f, 0.f};
-      if (g >= 0 && g < y2n) w = *(const v4f *)(yb + g);
-      *(LP4)(sp + s) = w;
-    }
+  const int64_t g0 = 2 * m0 - kPcK2Left - (ZOOM == 4 ? kPc4Q0 : kPcQ0);  // y2 entry of span sample 0
+  const v2f *yb = y2 + f * y2s;
+  for (int s = 2 * t; s < kPcK2Span; s += 512) {
+    const int64_t g = g0 + s;  // even: a pair is wholly inside or outside [0, y2n)
+    v4f w = v4f{0.f, 0.f, 0.f, 0.f};
+    if (g >= 0 && g < y2n) w = *(const v4f *)(yb + g);
+    *(LP4)(sp + s) = w;
   }
   __syncthreads();
   v2f v[kPcOwnBlk];
@@ -544,12 +514,11 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
 #pragma unroll
     for (int r = 0; r < 9; ++r) u[r] = sp[18 * t + 2 * r + 304];
   } else {
-    // zoom 8: g2 (57 taps) on z2; zoom 4: g1 (41 taps) on z1; zoom 2: g (25 taps) on z
-    constexpr int G = ZOOM == 2 ? kPc2G : ZOOM == 4 ? kPc4G1 : kPcG2;
+    // zoom 8: g2 (57 taps) on z2; zoom 4: g1 (41 taps) on z1
+    constexpr int G = ZOOM == 4 ? kPc4G1 : kPcG2;
     const auto taps = [&]() {
       if constexpr (ZOOM == 8) return tab->g2;
-      else if constexpr (ZOOM == 4) return tab->g1;
-      else return tab->g;
+      else return tab->g1;
     };
     const LP zb = sp + 18 * t + (kPcK2Left - 2 * kU3Base) - (G - 1) / 2;
 #pragma unroll
@@ -1040,8 +1009,8 @@ hipError_t launch_pc_fir(const InDesc &in, const float2 *lo, float2 *y2, int64_t
 hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int64_t n3,
                           int frames, const PcTab *tab, hipStream_t st) {
   const dim3 grid((unsigned)((n3 + kPcK2M - 1) / kPcK2M), frames);
-  hipLaunchKernelGGL((pc::pc_tail_kernel<8>), grid, dim3(256), 0, st, (const v2f *)y2, y2_stride,
-                     y2_stride, (v2f *)out, n3, (pc::CT)tab, InDesc{}, (const v2f *)nullptr);
+  hipLaunchKernelGGL(pc::pc_tail_kernel<8>, grid, dim3(256), 0, st, (const v2f *)y2, y2_stride,
+                     y2_stride, (v2f *)out, n3, (pc::CT)tab);
   return hipGetLastError();
 }
 
@@ -1056,29 +1025,8 @@ hipError_t launch_pc4_fir(const InDesc &in, const float2 *lo, float2 *y1, int64_
 hipError_t launch_pc4_tail(const float2 *y1, int64_t y1_stride, int64_t y1n, float2 *out, int64_t n2,
                            int frames, const PcTab4 *tab, hipStream_t st) {
   const dim3 grid((unsigned)((n2 + kPcK2M - 1) / kPcK2M), frames);
-  hipLaunchKernelGGL((pc::pc_tail_kernel<4>), grid, dim3(256), 0, st, (const v2f *)y1, y1_stride, y1n,
-                     (v2f *)out, n2, (pc::CT4)tab, InDesc{}, (const v2f *)nullptr);
-  return hipGetLastError();
-}
-
-#define PC_LAUNCH_TAIL2(DT, fl, ...)                                                            \
-  do {                                                                                           \
-    if (fl) hipLaunchKernelGGL((pc::pc_tail_kernel<2, DT, 1>), __VA_ARGS__);                     \
-    else hipLaunchKernelGGL((pc::pc_tail_kernel<2, DT, 0>), __VA_ARGS__);                        \
-  } while (0)
-hipError_t launch_pc2_tail(const InDesc &in, const float2 *lo, float2 *out, int64_t n1, int frames,
-                           const PcTab2 *tab, hipStream_t st) {
-  const dim3 grid((unsigned)((n1 + kPcK2M - 1) / kPcK2M), frames);
-  const bool fl = in.flip != 0;
-#define PC_TAIL2_ARGS grid, dim3(256), 0, st, (const v2f *)nullptr, (int64_t)0, (int64_t)0, (v2f *)out, n1, \
-                      (pc::CT2)tab, in, (const v2f *)lo
-  switch (in.dtype) {
-    case kInC64: PC_LAUNCH_TAIL2(kInC64, fl, PC_TAIL2_ARGS); break;
-    case kInC32H: PC_LAUNCH_TAIL2(kInC32H, fl, PC_TAIL2_ARGS); break;
-    case kInCU8: PC_LAUNCH_TAIL2(kInCU8, fl, PC_TAIL2_ARGS); break;
-    default: PC_LAUNCH_TAIL2(kInF32R, fl, PC_TAIL2_ARGS); break;
-  }
-#undef PC_TAIL2_ARGS
+  hipLaunchKernelGGL(pc::pc_tail_kernel<4>, grid, dim3(256), 0, st, (const v2f *)y1, y1_stride, y1n,
+                     (v2f *)out, n2, (pc::CT4)tab);
   return hipGetLastError();
 }
 

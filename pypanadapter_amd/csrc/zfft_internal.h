@@ -215,26 +215,6 @@ hipError_t launch_pc4_tail(const float2 *y1, int64_t y1_stride, int64_t y1n, flo
 __host__ __device__ constexpr int pc4_ap_levels(int s) { return s == 0 ? 3 : s <= 2 ? 2 : s <= 4 ? 1 : 0; }
 __host__ __device__ constexpr int pc4_ap_dcut(int) { return kPcApBlk; }
 bool pc_build_tables4(PcTab4 &tab);
-// Zoom 2 (one stage) as tiles (pc2_tail_kernel, path 4): the stage's two slowest sections
-// stay at its own rate -- the input rate -- and the other two move to the output rate:
-//   z = S(z) S(1/z) x               the own-rate sections (zoom 8's own[]: radius .808, .935)
-//   u = (g * z)|2                   FIR (25 taps: N D{0,1}(-z), zero phase)
-//   out = A(w) A(1/w) u             D2's sections 0, 1 (radius <= .465) at rate 1/2
-// with the tail kernel's span geometry (own-rate span 2 m0 - 560 .. + 5376 per 2048 outputs)
-// read straight from the mixed input.  Moving all four sections to rate 1/2 instead (one FIR,
-// no own-rate recurrence) amplifies the FIR's fp32 rounding to ~1e-4.
-constexpr int kPc2G = 25, kPc2Ap = 2;
-struct PcTab2 {
-  float g[28];                      // zero-phase FIR taps (centred)
-  PcSec own[kPcOwn];                // own-rate sections (those of PcTab: B = 21)
-  float own_x[kPcOwn][64][4];
-  PcSec ap[kPc2Ap];                 // B = 10, slowest first
-};
-__host__ __device__ constexpr int pc2_ap_levels(int) { return 2; }
-__host__ __device__ constexpr int pc2_ap_dcut(int) { return kPcApBlk; }
-bool pc_build_tables2(PcTab2 &tab);
-hipError_t launch_pc2_tail(const InDesc &in, const float2 *lo, float2 *out, int64_t n1, int frames,
-                           const PcTab2 *tab, hipStream_t st);
 // Frame-end maps, out[m] += sum_k U[m][k] (sum_j V[j][k] x[j]) (left: m, j from the start;
 // right: from the end), rank r.
 struct PcEdge {

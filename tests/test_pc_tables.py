@@ -226,72 +226,3 @@ def test_pc4_model_plus_edge_maps_is_reference_decimate(L):
     out[len(out) - CR.shape[0]:] += (CR @ x[::-1][:CR.shape[1]])[::-1]
     err = np.abs(out - ref).max() / np.abs(ref).max()
     assert err < 2e-7, err
-
-
-# ---- zoom 2 (one stage; PcTab2, pc_tail_kernel<2>) ----
-
-def _model2():
-    s = _secs()
-    n9 = SOS[0, 0] * np.array([1, 8, 28, 56, 70, 56, 28, 8, 1.0])
-    f = _conv(n9, _neg(_poly(*s[0], [0, 1])))
-    own = [(s[0][0][i], s[0][1][i]) for i in (2, 3)]
-    ap = sorted([(s[1][0][i], s[1][1][i]) for i in (0, 1)], key=lambda p: -p[1])
-    return np.convolve(f, f[::-1]), own, ap
-
-
-def _edge2(side, lm, shipped=False):
-    if shipped:
-        v = _call(17, 0 if side == 0 else 1 + lm)
-        R, J, r = int(v[0]), int(v[1]), int(v[2])
-        return v[3:3 + R * r].reshape(R, r), v[3 + R * r:3 + R * r + J * r].reshape(r, J).T
-    v = _call(15 + side, lm)
-    R, J, r = int(v[0]), int(v[1]), int(v[2])
-    return v[3:3 + R * r].reshape(R, r), v[3 + R * r:3 + R * r + J * r].reshape(J, r)
-
-
-def test_pc2_taps_and_sections():
-    """Zoom 2's FIR is |N D{0,1}(-z)|^2 (25 taps) and its output-rate sections the stage's fast
-    pair squared (D2 sections 0, 1), slowest first; the own-rate sections are zoom 8's."""
-    g, _, ap = _model2()
-    v = _call(6)
-    assert v.size == 25 + 4
-    np.testing.assert_allclose(v[:25], g, rtol=0, atol=6e-8 * np.abs(g).max())  # fp32 taps
-    np.testing.assert_allclose(v[25:].reshape(2, 2), np.array(ap), rtol=1e-7)
-
-
-@pytest.mark.parametrize("side,lm", [(0, 0), (1, 0), (1, 1)])
-def test_pc2_shipped_edge_maps_are_the_builders(side, lm):
-    Ub, Vb = _edge2(side, lm)
-    Us, Vs = _edge2(side, lm, shipped=True)
-    assert Ub.shape == Us.shape and Vb.shape == Vs.shape
-    np.testing.assert_array_equal(Us, Ub)
-    np.testing.assert_array_equal(Vs, Vb)
-
-
-@pytest.mark.parametrize("L", [16384, 16385, 20006, 262144 + 1])
-def test_pc2_model_plus_edge_maps_is_reference_decimate(L):
-    """Zoom 2 (the UI's default fft_ratio, S:1497): the one-stage model -- own-rate sections at
-    the input rate, the 25-tap FIR, 2 output-rate sections -- and its shipped frame-end maps
-    give scipy's decimate(x, 2) for both L mod 2."""
-    g, own, ap = _model2()
-    rng = np.random.default_rng(L + 2)
-    x = rng.standard_normal(L) + 1j * rng.standard_normal(L)
-    x += 3 * np.exp(2j * np.pi * 0.041 * np.arange(L))
-    ref = ss.decimate(x, 2)
-    pad = 4096
-    y = np.concatenate([np.zeros(pad), x, np.zeros(pad)])
-    so = np.array([[1, 0, 0, 1, a1, a2] for a1, a2 in own])
-    y = ss.sosfilt(so, ss.sosfilt(so, y)[::-1])[::-1]
-    y = np.convolve(y, g)[12::2][:len(y) // 2]
-    sa = np.array([[1, 0, 0, 1, a1, a2] for a1, a2 in ap])
-    out = ss.sosfilt(sa, ss.sosfilt(sa, y)[::-1])[::-1][pad // 2:pad // 2 + (L + 1) // 2]
-    assert out.shape == ref.shape
-    inner = np.abs(out - ref)[300:-300].max() / np.abs(ref).max()
-    assert inner < 1e-12, inner
-    UL, VL = _edge2(0, L % 2, shipped=True)
-    UR, VR = _edge2(1, L % 2, shipped=True)
-    CL, CR = UL @ VL.T, UR @ VR.T
-    out[:CL.shape[0]] += CL @ x[:CL.shape[1]]
-    out[len(out) - CR.shape[0]:] += (CR @ x[::-1][:CR.shape[1]])[::-1]
-    err = np.abs(out - ref).max() / np.abs(ref).max()
-    assert err < 2e-7, err
