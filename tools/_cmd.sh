@@ -1,6 +1,6 @@
 # Scratch GPU command of the current session (run as: gpurun -- 'bash tools/_cmd.sh'):
-# the final-sources session: GPU tests, smoke, the driver's bench line, rocprofv3 kernel
-# trace, PMC traffic and SQ counters (stamped into profiles/), every BASELINE config.
+# A/B: odd walk workgroups at s_setprio 1 / 3 against none.
 set -u
 export TMPDIR=/tmp
-bash tools/gpu_session.sh r05fin3 tests smoke driver prof pmc sq stamp cfgs
+V=pypanadapter_amd/lib/variants
+AB_REPS=3 bash tools/ab.sh r05x base=$V/libzfft_base.so wgp1=$V/libzfft_wgp1.so wgp3=$V/libzfft_wgp3.so
