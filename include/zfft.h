@@ -202,15 +202,16 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
 
 /* Decimator schedule: 0 = automatic -- for zoom 8 and frames of >= 16384 samples 4 below
  * 4096 frames per call and 5 from there (zoom >= 16: the same for the first three stages;
- * zoom 4: 4 below 1024 frames per call); otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
+ * zoom 4: 4 below 1024 frames per call, zoom 2 below 512); otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
  * samples, else 2 for batches of >= 2^27 samples whose frames are long enough for the edge
  * windows, else 1 -- e.g. one frame per call, the reference's use.  Each batch of a
  * zfft_process call is judged by its own frame count (host calls are split into batches of
  * about 1 GiB of input -- 418 cfg2 frames -- so from host memory path 5 is reached only by
  * forcing it; zfft_process_device judges the whole call); crossovers measured by
  * tools/sweep_schedule.py (profiles/r04v/sweep_schedule.json).  Default tolerance: the
- * automatic zoom-8 choice (PC, paths 4/5, also for one frame per call) gives the float64
- * reference's decimated IQ within 7e-6 of its peak (measured 2-5.3e-6; path 1: 2e-6).
+ * automatic PC choices (zoom 8 at every batch, zoom 4 below 1024 frames per call, zoom 2
+ * below 512, the head of zoom >= 16) give the float64 reference's decimated IQ within 7e-6 of its peak
+ * (measured 2-5.3e-6; path 1: 2e-6).
  * 1 = blocked warm-up passes in the reference order (frames split over many waves),
  * 2 = blocked, fused commuted-order interior + exact edge windows, 3 = XA tiles (one wave per
  * frame and stage: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned;
@@ -222,7 +223,9 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * stays on chip; automatic from 4096 frames per call); at zoom 4, path 5 is the two-stage
  * form of the walk (FIR, own-rate sections at rate 1/2, 41-tap FIR, 6 output-rate sections;
  * on request only: XA is faster there) and path 4 its tiles (automatic below 1024 frames per
- * call, XA from there); at zoom >= 16, paths 4 / 5 run PC (tiles / walk) for the
+ * call, XA from there); at zoom 2, paths 4 / 5 run one-stage tiles in XA's factorisation (the
+ * 4 sections forward at the input rate, a 25-tap FIR, their squares backward at half rate;
+ * automatic below 512 frames per call); at zoom >= 16, paths 4 / 5 run PC (tiles / walk) for the
  * first three stages and XA for the rest on its 1/8-rate output -- the automatic choice
  * wherever XA would take the batch (zoom 16 on cfg2's frames: 5.23 against XA's 6.35 ms per
  * 4096 frames).  Path 3

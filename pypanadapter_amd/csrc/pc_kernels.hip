@@ -93,6 +93,7 @@ typedef v2f __attribute__((address_space(3))) *LP;
 typedef v4f __attribute__((address_space(3))) *LP4;
 typedef const PcTab __attribute__((address_space(4))) *CT;
 typedef const PcTab4 __attribute__((address_space(4))) *CT4;
+typedef const PcTab2 __attribute__((address_space(4))) *CT2;
 typedef const PcSec __attribute__((address_space(4))) &CS;
 
 __device__ __forceinline__ v2f shup(v2f v, int d) {
@@ -231,6 +232,7 @@ __device__ __forceinline__ void load_pair(const InDesc &in, int64_t f, int64_t n
 //   y2[q] = sum_t g1[t + 24] y1[2q - t]                            (4 per thread)
 template <int ZOOM> struct PcTabOf { typedef CT T; };
 template <> struct PcTabOf<4> { typedef CT4 T; };
+template <> struct PcTabOf<2> { typedef CT2 T; };
 // ZOOM = 4: FIR alpha only, y1 [m_s, m_s + 2048), m_s = kPc4Q0 + 2048 tile, from the mixed
 // input x[2 m_s - 16, + 4128) -- the same input tile and thread map -- written to y2 (= y1 here)
 template <int DT, int FLIP, int ZOOM>
@@ -463,6 +465,13 @@ __device__ __forceinline__ void ap_cascade(v2f (&a)[kPcApBlk], CT4 tab0, int lan
   sec_run<kPcApBlk, pc4_ap_levels(S), pc4_ap_dcut(S), UP>(a, tab->ap[S], lane);
   if constexpr (S + 1 < kPc4Ap) ap_cascade<S + 1, UP>(a, tab, lane);
 }
+// zoom 2's (PcTab2::ap, 4 sections)
+template <int S, bool UP>
+__device__ __forceinline__ void ap_cascade(v2f (&a)[kPcApBlk], CT2 tab0, int lane) {
+  const CT2 tab = fresh(tab0);
+  sec_run<kPcApBlk, pc2_ap_levels(S), pc2_ap_dcut(S), UP>(a, tab->ap[S], lane);
+  if constexpr (S + 1 < kPc2Ap) ap_cascade<S + 1, UP>(a, tab, lane);
+}
 
 constexpr int kU3 = 256 * 9;                   // FIR gamma outputs per tile (9 per thread)
 constexpr int kU3Base = 128;                    // u3 index k <-> output m0 - 128 + k
@@ -474,29 +483,57 @@ static_assert(kU3Base - kPcApHalo + 3 * (kPcK2M / 4) + kApWave <= kU3, "u3 cover
 
 // One tile: outputs [m0, m0 + 2048), m0 = 2048 tile, from y2 over [2 m0 - 560, + 5376).
 // ZOOM = 4: the same on y1 (stored from kPc4Q0) with zoom 4's FIR g1 and output-rate sections.
-template <int ZOOM>
+// ZOOM = 2: XA's factorisation -- the own-rate signal is the mixed input itself (span sample
+// s = input sample 2 m0 - 560 + s, zero outside the frame), D's 4 sections causal only, the
+// 25-tap FIR M (z^-8 .. z^16), D2's 4 sections anticausal only.
+template <int ZOOM, int DT = kInC64, int FLIP = 0>
 __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s, int64_t y2n,
-                                                      v2f *out, int64_t n3, typename PcTabOf<ZOOM>::T tab) {
+                                                      v2f *out, int64_t n3, typename PcTabOf<ZOOM>::T tab,
+                                                      InDesc in, const v2f *lo) {
   __shared__ v4f sp4[kPcK2Span / 2];
   __shared__ v4f scr4[4 * 4];
   const LP sp = (LP)sp4;
   const LP scr = (LP)scr4;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t f = blockIdx.y, m0 = (int64_t)kPcK2M * blockIdx.x;
-  const int64_t g0 = 2 * m0 - kPcK2Left - (ZOOM == 4 ? kPc4Q0 : kPcQ0);  // y2 entry of span sample 0
-  const v2f *yb = y2 + f * y2s;
-  for (int s = 2 * t; s < kPcK2Span; s += 512) {
-    const int64_t g = g0 + s;  // even: a pair is wholly inside or outside [0, y2n)
-    v4f w = v4f{0.f, 0.f, 0.f, 0.f};
-    if (g >= 0 && g < y2n) w = *(const v4f *)(yb + g);
-    *(LP4)(sp + s) = w;
+  if constexpr (ZOOM == 2) {
+    const int64_t n0 = 2 * m0 - kPcK2Left, L = in.len;
+    const v2f *lor = lo_row(lo, in, f);
+    for (int s = 2 * t; s < kPcK2Span; s += 512) {
+      const int64_t n = n0 + s;
+      v2f a = splat(0.f), b = splat(0.f);
+      if (n >= 0 && n + 2 <= L) {
+        load_pair<DT, FLIP>(in, f, n, a, b);
+        a = cmul2(a, lor[n]);
+        b = cmul2(b, lor[n + 1]);
+      } else {
+        if (n >= 0 && n < L) a = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
+        if (n + 1 >= 0 && n + 1 < L) b = cmul2(load_in_t<DT, FLIP>(in, f, n + 1), lor[n + 1]);
+      }
+      *(LP4)(sp + s) = cat(a, b);
+    }
+  } else {
+    const int64_t g0 = 2 * m0 - kPcK2Left - (ZOOM == 4 ? kPc4Q0 : kPcQ0);  // y2 entry of span sample 0
+    const v2f *yb = y2 + f * y2s;
+    for (int s = 2 * t; s < kPcK2Span; s += 512) {
+      const int64_t g = g0 + s;  // even: a pair is wholly inside or outside [0, y2n)
+      v4f w = v4f{0.f, 0.f, 0.f, 0.f};
+      if (g >= 0 && g < y2n) w = *(const v4f *)(yb + g);
+      *(LP4)(sp + s) = w;
+    }
   }
   __syncthreads();
   v2f v[kPcOwnBlk];
 #pragma unroll
   for (int k = 0; k < kPcOwnBlk; ++k) v[k] = sp[kPcOwnBlk * t + k];
-  // own-rate sections, causal then anticausal (warm-up: the span's first / last 330)
-  if constexpr (!(kKo & 1)) {
+  // own-rate sections, causal then anticausal (warm-up: the span's first / last 330); zoom 2:
+  // D's four, causal only (XA's forward pass, warm-up: the span's first 296)
+  if constexpr (ZOOM == 2) {
+    sec_block<kPcOwnBlk, pc2_own_levels(0), kPcOwnBlk, true, true, true, 0>(v, tab, scr, lane, wave);
+    sec_block<kPcOwnBlk, pc2_own_levels(1), kPcOwnBlk, true, true, true, 1>(v, tab, scr + 8, lane, wave);
+    sec_block<kPcOwnBlk, pc2_own_levels(2), kPcOwnBlk, true, true, true, 2>(v, tab, scr + 16, lane, wave);
+    sec_block<kPcOwnBlk, pc2_own_levels(3), kPcOwnBlk, true, true, true, 3>(v, tab, scr + 24, lane, wave);
+  } else if constexpr (!(kKo & 1)) {
     sec_block<kPcOwnBlk, pc_own_levels(0), kPcOwnBlk, true, true, true, 0>(v, tab, scr, lane, wave);
     sec_block<kPcOwnBlk, pc_own_levels(1), kPcOwnBlk, true, true, true, 1>(v, tab, scr + 8, lane, wave);
     sec_block<kPcOwnBlk, pc_own_levels(0), kPcOwnBlk, false, true, true, 0>(v, tab, scr + 16, lane, wave);
@@ -514,13 +551,16 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
 #pragma unroll
     for (int r = 0; r < 9; ++r) u[r] = sp[18 * t + 2 * r + 304];
   } else {
-    // zoom 8: g2 (57 taps) on z2; zoom 4: g1 (41 taps) on z1
-    constexpr int G = ZOOM == 4 ? kPc4G1 : kPcG2;
+    // zoom 8: g2 (57 taps) on z2; zoom 4: g1 (41 taps) on z1; zoom 2: g (25 taps) on z
+    constexpr int G = ZOOM == 2 ? kPc2G : ZOOM == 4 ? kPc4G1 : kPcG2;
     const auto taps = [&]() {
       if constexpr (ZOOM == 8) return tab->g2;
-      else return tab->g1;
+      else if constexpr (ZOOM == 4) return tab->g1;
+      else return tab->g;
     };
-    const LP zb = sp + 18 * t + (kPcK2Left - 2 * kU3Base) - (G - 1) / 2;
+    // tap u multiplies z[2 m + u - C]: centred (C = (G - 1) / 2), or M's z^-8 .. z^16 at zoom 2
+    constexpr int C = ZOOM == 2 ? -kPc2M0 : (G - 1) / 2;
+    const LP zb = sp + 18 * t + (kPcK2Left - 2 * kU3Base) - C;
 #pragma unroll
     for (int p = 0; p < (G + 17) / 2; ++p) {
       const int j = 2 * p;
@@ -535,13 +575,16 @@ __global__ void __launch_bounds__(256) pc_tail_kernel(const v2f *y2, int64_t y2s
   for (int r = 0; r < 9; ++r) sp[9 * t + r] = u[r];
   __syncthreads();
   // output-rate sections: wave q takes outputs [512 q, + 512) with 64-sample halos, u3
-  // index k = 64 + 512 q + 10 lane + i
+  // index k = 64 + 512 q + 10 lane + i; zoom 2: anticausal only (XA's backward pass at half
+  // rate), so no lower halo and a 128-sample upper one (.874^128 = 3.2e-8)
   {
     v2f a[kPcApBlk];
-    const int k0 = kU3Base - kPcApHalo + (kPcK2M / 4) * wave + kPcApBlk * lane;
+    const int k0 = kU3Base - (ZOOM == 2 ? 0 : kPcApHalo) + (kPcK2M / 4) * wave + kPcApBlk * lane;
 #pragma unroll
     for (int i = 0; i < kPcApBlk; ++i) a[i] = sp[k0 + i];
-    if constexpr (!(kKo & 4)) {
+    if constexpr (ZOOM == 2) {
+      ap_cascade<0, false>(a, tab, lane);
+    } else if constexpr (!(kKo & 4)) {
       ap_cascade<0, true>(a, tab, lane);
       ap_cascade<0, false>(a, tab, lane);
     }
@@ -1009,8 +1052,8 @@ hipError_t launch_pc_fir(const InDesc &in, const float2 *lo, float2 *y2, int64_t
 hipError_t launch_pc_tail(const float2 *y2, int64_t y2_stride, float2 *out, int64_t n3,
                           int frames, const PcTab *tab, hipStream_t st) {
   const dim3 grid((unsigned)((n3 + kPcK2M - 1) / kPcK2M), frames);
-  hipLaunchKernelGGL(pc::pc_tail_kernel<8>, grid, dim3(256), 0, st, (const v2f *)y2, y2_stride,
-                     y2_stride, (v2f *)out, n3, (pc::CT)tab);
+  hipLaunchKernelGGL((pc::pc_tail_kernel<8>), grid, dim3(256), 0, st, (const v2f *)y2, y2_stride,
+                     y2_stride, (v2f *)out, n3, (pc::CT)tab, InDesc{}, (const v2f *)nullptr);
   return hipGetLastError();
 }
 
@@ -1025,8 +1068,29 @@ hipError_t launch_pc4_fir(const InDesc &in, const float2 *lo, float2 *y1, int64_
 hipError_t launch_pc4_tail(const float2 *y1, int64_t y1_stride, int64_t y1n, float2 *out, int64_t n2,
                            int frames, const PcTab4 *tab, hipStream_t st) {
   const dim3 grid((unsigned)((n2 + kPcK2M - 1) / kPcK2M), frames);
-  hipLaunchKernelGGL(pc::pc_tail_kernel<4>, grid, dim3(256), 0, st, (const v2f *)y1, y1_stride, y1n,
-                     (v2f *)out, n2, (pc::CT4)tab);
+  hipLaunchKernelGGL((pc::pc_tail_kernel<4>), grid, dim3(256), 0, st, (const v2f *)y1, y1_stride, y1n,
+                     (v2f *)out, n2, (pc::CT4)tab, InDesc{}, (const v2f *)nullptr);
+  return hipGetLastError();
+}
+
+#define PC_LAUNCH_TAIL2(DT, fl, ...)                                                            \
+  do {                                                                                           \
+    if (fl) hipLaunchKernelGGL((pc::pc_tail_kernel<2, DT, 1>), __VA_ARGS__);                     \
+    else hipLaunchKernelGGL((pc::pc_tail_kernel<2, DT, 0>), __VA_ARGS__);                        \
+  } while (0)
+hipError_t launch_pc2_tail(const InDesc &in, const float2 *lo, float2 *out, int64_t n1, int frames,
+                           const PcTab2 *tab, hipStream_t st) {
+  const dim3 grid((unsigned)((n1 + kPcK2M - 1) / kPcK2M), frames);
+  const bool fl = in.flip != 0;
+#define PC_TAIL2_ARGS grid, dim3(256), 0, st, (const v2f *)nullptr, (int64_t)0, (int64_t)0, (v2f *)out, n1, \
+                      (pc::CT2)tab, in, (const v2f *)lo
+  switch (in.dtype) {
+    case kInC64: PC_LAUNCH_TAIL2(kInC64, fl, PC_TAIL2_ARGS); break;
+    case kInC32H: PC_LAUNCH_TAIL2(kInC32H, fl, PC_TAIL2_ARGS); break;
+    case kInCU8: PC_LAUNCH_TAIL2(kInCU8, fl, PC_TAIL2_ARGS); break;
+    default: PC_LAUNCH_TAIL2(kInF32R, fl, PC_TAIL2_ARGS); break;
+  }
+#undef PC_TAIL2_ARGS
   return hipGetLastError();
 }
 

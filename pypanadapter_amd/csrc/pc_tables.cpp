@@ -231,8 +231,8 @@ std::vector<double> model_hz_build(int K) {
   }
 }
 const std::vector<double> &model_hz(int K) {
-  static const std::vector<double> H2 = model_hz_build(2), H3 = model_hz_build(3);
-  return K == 2 ? H2 : H3;
+  static const std::vector<double> H1 = model_hz_build(1), H2 = model_hz_build(2), H3 = model_hz_build(3);
+  return K == 1 ? H1 : K == 2 ? H2 : H3;
 }
 
 // C[m][j] = (exact - model)(e_j) at output m of K stages; side 0 from the frame start, side 1
@@ -353,6 +353,38 @@ bool pc_build_tables4(PcTab4 &tab) {
   return true;
 }
 
+bool pc_build_tables2(PcTab2 &tab) {
+  std::memset(&tab, 0, sizeof(tab));
+  const Lev &l = levels();
+  // M(z) = N(z) N(1/z) D(-1/z): with N(1/z) and D(-1/z) written as the reversed lists of N and
+  // D(-z) (entry j <-> z^(8 - j)), entry i of the product list is the power z^(16 - i)
+  const Poly dneg = neg(sec_poly(l.d[0], {0, 1, 2, 3}));  // D(-z): entry k <-> z^-k
+  const Poly nrev(l.n9.rbegin(), l.n9.rend());
+  const Poly drev(dneg.rbegin(), dneg.rend());
+  const Poly m = conv(l.n9, conv(nrev, drev));
+  if ((int)m.size() != kPc2G) return false;
+  for (int i = 0; i < kPc2G; ++i) tab.g[i] = (float)m[16 - (i + kPc2M0)];  // z^(i - 8)
+  std::vector<std::pair<double, double>> own, ap;
+  for (int k = 0; k < 4; ++k) own.emplace_back(l.d[0].a1[k], l.d[0].a2[k]), ap.emplace_back(l.d[1].a1[k], l.d[1].a2[k]);
+  auto slow_first = [](auto &a, auto &b) { return a.second > b.second; };
+  std::stable_sort(own.begin(), own.end(), slow_first);
+  std::stable_sort(ap.begin(), ap.end(), slow_first);
+  for (int s = 0; s < kPc2Own; ++s) {
+    const double a1 = own[s].first, a2 = own[s].second;
+    if (!sec_tables(a1, a2, kPcOwnBlk, pc2_own_levels(s), kPcOwnBlk, tab.own[s])) return false;
+    const M2 A = {{-a1, -a2}, {1.0, 0.0}};
+    for (int i = 0; i < 64; ++i) {
+      M2 P;
+      pow2(A, kPcOwnBlk * (i + 1), P);
+      for (int q = 0; q < 4; ++q) tab.own_x[s][i][q] = (float)P[q / 2][q % 2];
+    }
+  }
+  for (int s = 0; s < kPc2Ap; ++s)
+    if (!sec_tables(ap[s].first, ap[s].second, kPcApBlk, pc2_ap_levels(s), pc2_ap_dcut(s), tab.ap[s]))
+      return false;
+  return true;
+}
+
 bool pc_edge_map(int side, int lmod8, PcEdge &out) { return pc_edge_map_k(3, side, lmod8, out); }
 
 bool pc_edge_map_k(int K, int side, int lmod, PcEdge &out) {
@@ -438,7 +470,9 @@ bool pc_edge_map_k(int K, int side, int lmod, PcEdge &out) {
 //   2 / 3: left / right edge map for L mod 8 = arg built now (fp64): R, J, r then U (R x r), V (J x r);
 //   4: the shipped constant map arg of pc_edge_maps.h: R, J, r then U (R x r), V^T (r x J);
 //   5: zoom 4 FIR taps g0 | g1 (74 floats); 12 / 13: zoom-4 left / right map for L mod 4 = arg
-//   built now; 14: the shipped zoom-4 map arg.
+//   built now; 14: the shipped zoom-4 map arg; 6: zoom 2 FIR taps M + its input-rate and
+//   output-rate sections' a1, a2 (41 floats); 15 / 16: zoom-2 left / right map for L mod 2 = arg
+//   built now; 17: the shipped zoom-2 map arg.
 extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
   using namespace zfft;
   if (what == 0 || what == 1) {
@@ -465,10 +499,23 @@ extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
     std::memcpy(out + kPcG0, t.g1, kPc4G1 * 4);
     return kPcG0 + kPc4G1;
   }
-  if (what == 12 || what == 13) {  // zoom 4: left / right map for L mod 4 = arg, built now
-    PcEdge e;
+  if (what == 6) {  // zoom 2: FIR taps M (25 floats, z^-8 first), then the input-rate and the
+                    // output-rate sections' a1, a2 (4 + 4 pairs)
+    PcTab2 t;
+    if (!pc_build_tables2(t)) return -1;
+    const int n = kPc2G + 2 * (kPc2Own + kPc2Ap);
+    if (cap < n) return -2;
+    std::memcpy(out, t.g, kPc2G * 4);
+    float *o = out + kPc2G;
+    for (int s = 0; s < kPc2Own; ++s) *o++ = t.own[s].a1, *o++ = t.own[s].a2;
+    for (int s = 0; s < kPc2Ap; ++s) *o++ = t.ap[s].a1, *o++ = t.ap[s].a2;
+    return n;
+  }
+  if (what == 12 || what == 13 || what == 15 || what == 16) {  // zoom 4 (12, 13) / zoom 2 (15, 16):
+    PcEdge e;                                                  // left / right map, built now
+    const int K = what < 15 ? 2 : 1;
     try {
-      if (!pc_edge_map_k(2, what - 12, arg & 3, e)) return -1;
+      if (!pc_edge_map_k(K, (what - 12) % 3, arg & ((1 << K) - 1), e)) return -1;
     } catch (...) {
       return -4;
     }
@@ -481,10 +528,11 @@ extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
     std::copy(e.V.begin(), e.V.end(), out + 3 + e.R * e.r);
     return n;
   }
-  if (what == 4 || what == 14) {  // the shipped constant map arg (0 start, 1 + k end for L mod
-                                  // 2^K = k): zoom 8 (4), zoom 4 (14)
-    if (arg < 0 || arg >= (what == 4 ? kPcEdgeMaps : kPcEdge4Maps)) return -3;
-    const PcEdgeConst &m = what == 4 ? kPcEdgeIdx[arg] : kPcEdge4Idx[arg];
+  if (what == 4 || what == 14 || what == 17) {  // the shipped constant map arg (0 start, 1 + k
+                                                // end for L mod 2^K = k): zoom 8, 4, 2
+    const int nmaps = what == 4 ? kPcEdgeMaps : what == 14 ? kPcEdge4Maps : kPcEdge2Maps;
+    if (arg < 0 || arg >= nmaps) return -3;
+    const PcEdgeConst &m = what == 4 ? kPcEdgeIdx[arg] : what == 14 ? kPcEdge4Idx[arg] : kPcEdge2Idx[arg];
     const int n = 3 + m.R * m.r + m.J * m.r;
     if (cap < n) return -2;
     out[0] = (float)m.R;

@@ -215,6 +215,28 @@ hipError_t launch_pc4_tail(const float2 *y1, int64_t y1_stride, int64_t y1n, flo
 __host__ __device__ constexpr int pc4_ap_levels(int s) { return s == 0 ? 3 : s <= 2 ? 2 : s <= 4 ? 1 : 0; }
 __host__ __device__ constexpr int pc4_ap_dcut(int) { return kPcApBlk; }
 bool pc_build_tables4(PcTab4 &tab);
+// Zoom 2 (one stage) as tiles (the tail kernel on the mixed input, path 4; few frames per call):
+// XA's factorisation in the tail kernel's span geometry --
+//   v = x / D(z)                    the stage's 4 sections, causal, at the input rate (B = 21)
+//   u = (M * v)|2                   M = N(z) N(1/z) D(-1/z): 25 taps, z^-8 .. z^16
+//   out = u / D2(1/w)               D2's 4 sections, anticausal, at rate 1/2 (radius <= .874)
+// -- each pole once per direction.  The zero-phase form with the two slow sections both ways
+// at the input rate (and the other poles at rate 1/2) missed the row gate on a band-edge tone
+// (|damp| 1.9e-5); this one is XA's arithmetic.
+constexpr int kPc2G = 25, kPc2Ap = 4, kPc2Own = 4;
+constexpr int kPc2M0 = -8;                 // power of z of M's first tap
+struct PcTab2 {
+  float g[28];                      // M_(i + kPc2M0), i < 25
+  PcSec own[kPc2Own];               // D's sections at the input rate, B = 21, slowest first
+  float own_x[kPc2Own][64][4];      // A^(21 (i + 1)) for lane i (cross-wave step)
+  PcSec ap[kPc2Ap];                 // D2's sections at rate 1/2, B = 10, slowest first
+};
+__host__ __device__ constexpr int pc2_own_levels(int s) { return 4 - s; }
+__host__ __device__ constexpr int pc2_ap_levels(int s) { return 4 - s; }
+__host__ __device__ constexpr int pc2_ap_dcut(int) { return kPcApBlk; }
+bool pc_build_tables2(PcTab2 &tab);
+hipError_t launch_pc2_tail(const InDesc &in, const float2 *lo, float2 *out, int64_t n1, int frames,
+                           const PcTab2 *tab, hipStream_t st);
 // Frame-end maps, out[m] += sum_k U[m][k] (sum_j V[j][k] x[j]) (left: m, j from the start;
 // right: from the end), rank r.
 struct PcEdge {

@@ -406,6 +406,7 @@ struct zfft_plan {
   DevBuf edge, xk, xa_tab, tws, means, z4, winf;
   DevBuf pc_tab, pc_edge;  // PC decimator: PcTab; edge maps U0 V0 U1 V1 (floats)
   DevBuf pc_tab4;  // PC zoom 4: PcTab4
+  DevBuf pc_tab2;  // PC zoom 2: PcTab2
   DevBuf wparts;   // split DIF Welch: partial PSDs (frames x split x n_win floats)
   DevBuf lo1;      // unit LO table (the blocked passes after the PC head mix with it)
                            // (pc_edge: all nine maps of pc_edge_maps.h, uploaded once)
@@ -806,6 +807,15 @@ bool pc4_fits(const zfft_plan *p, int64_t L, int frames) {
 // 1.26, 1024: 1.64 / 1.56 -- XA, one wave per frame, needs about a thousand frames to fill the
 // chip.
 constexpr int kPc4TilesMaxFrames = 1024;
+// Zoom 2 (one stage): the tail kernel on the mixed input in XA's factorisation (D forward at
+// the input rate, the 25-tap FIR M, D2 backward at half rate), automatic below
+// 512 frames per call: cfg2's 299,008-sample frames, ms per call, tiles / XA (profiles/r05y):
+// 1 frame 0.048 / 0.89 (blocked passes 0.16), 64: 0.16 / 0.95 (0.28), 384: 0.85 / 1.18,
+// 1024: 2.05 / 1.53 -- equal near 640.
+constexpr int kPc2TilesMaxFrames = 512;
+bool pc2_fits(const zfft_plan *p, int64_t L, int frames) {
+  return p->K == 1 && L >= kPcMinL && frames <= 65535;
+}
 // Zoom >= 16: PC takes the first three stages (decimate x 3 exactly, frame-end maps included)
 // and XA the remaining K - 3 on its 1/8-rate output -- the reference's stages are applied one
 // after another (S:2096-2098), so the composition is the same cascade.
@@ -823,6 +833,14 @@ const PcTab *pc_host_tab() {
   }();
   return t.get();
 }
+const PcTab2 *pc_host_tab2() {
+  static const std::unique_ptr<PcTab2> t = [] {
+    std::unique_ptr<PcTab2> x(new PcTab2());
+    if (!pc_build_tables2(*x)) x.reset();
+    return x;
+  }();
+  return t.get();
+}
 const PcTab4 *pc_host_tab4() {
   static const std::unique_ptr<PcTab4> t = [] {
     std::unique_ptr<PcTab4> x(new PcTab4());
@@ -834,10 +852,14 @@ const PcTab4 *pc_host_tab4() {
 // The PC tables and all nine frame-end maps, uploaded on the plan's first PC call; nothing is
 // uploaded afterwards, so a change of L mod 8 between calls never waits on enqueued work.
 int ensure_pc(zfft_plan *p) {
-  if (p->pc_tab.p && p->pc_tab4.p && p->pc_edge.p) return ZFFT_OK;
+  if (p->pc_tab.p && p->pc_tab4.p && p->pc_tab2.p && p->pc_edge.p) return ZFFT_OK;
   const PcTab *t = pc_host_tab();
   const PcTab4 *t4 = pc_host_tab4();
-  if (!t || !t4) return fail(ZFFT_EINTERNAL, "PC tables: scan depth or correction length too short");
+  const PcTab2 *t2 = pc_host_tab2();
+  if (!t || !t4 || !t2) return fail(ZFFT_EINTERNAL, "PC tables: scan depth or correction length too short");
+  for (const PcEdgeConst &m : kPcEdge2Idx)
+    if (m.r > kPcEdgeRank || m.R > kPcEdgeR || m.R > 256)
+      return fail(ZFFT_EINTERNAL, "PC frame-end maps exceed the kernel's capacities");
   for (const PcEdgeConst &m : kPcEdgeIdx)
     if (m.r > kPcEdgeRank || m.R > kPcEdgeR || m.R > 256)
       return fail(ZFFT_EINTERNAL, "PC frame-end maps exceed the kernel's capacities");
@@ -848,6 +870,8 @@ int ensure_pc(zfft_plan *p) {
   if (e == hipSuccess) e = hipMemcpy(p->pc_tab.p, t, sizeof(PcTab), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = p->pc_tab4.ensure(sizeof(PcTab4));
   if (e == hipSuccess) e = hipMemcpy(p->pc_tab4.p, t4, sizeof(PcTab4), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = p->pc_tab2.ensure(sizeof(PcTab2));
+  if (e == hipSuccess) e = hipMemcpy(p->pc_tab2.p, t2, sizeof(PcTab2), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = p->pc_edge.ensure(sizeof(kPcEdgeData));
   if (e == hipSuccess) e = hipMemcpy(p->pc_edge.p, kPcEdgeData, sizeof(kPcEdgeData), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "PC table upload");
@@ -864,7 +888,13 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
   const int64_t n3 = n[K];
   const PcTab *tab = p->pc_tab.as<PcTab>();
   hipError_t e;
-  if (K == 2 && !walk) {  // zoom 4 as tiles: K1 (FIR alpha) -> y1 (ping) -> K2 -> out (pong)
+  if (K == 1) {  // zoom 2: the tail kernel straight on the mixed input
+    e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
+    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
+    e = launch_pc2_tail(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab2.as<PcTab2>(), st);
+    if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
+    mark(p, st, "pc_tail");
+  } else if (K == 2 && !walk) {  // zoom 4 as tiles: K1 (FIR alpha) -> y1 (ping) -> K2 -> out (pong)
     const int64_t y1s = (pc4_y1_len(L) + kPc4K1M - 1) / kPc4K1M * kPc4K1M;
     e = p->ping.ensure((size_t)frames * y1s * sizeof(float2));
     if (e == hipSuccess) e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
@@ -902,8 +932,10 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
   }
   // map 0 = frame start, 1 + (L mod 2^K) = frame end (pc_edge_maps.h)
   const float *eb = p->pc_edge.as<float>();
-  const PcEdgeConst &m0 = K == 2 ? kPcEdge4Idx[0] : kPcEdgeIdx[0];
-  const PcEdgeConst &m1 = K == 2 ? kPcEdge4Idx[1 + (L & 3)] : kPcEdgeIdx[1 + (L & 7)];
+  const PcEdgeConst &m0 = K == 1 ? kPcEdge2Idx[0] : K == 2 ? kPcEdge4Idx[0] : kPcEdgeIdx[0];
+  const PcEdgeConst &m1 = K == 1   ? kPcEdge2Idx[1 + (L & 1)]
+                          : K == 2 ? kPcEdge4Idx[1 + (L & 3)]
+                                   : kPcEdgeIdx[1 + (L & 7)];
   const float *const U[2] = {eb + m0.u, eb + m1.u};
   const float *const V[2] = {eb + m0.v, eb + m1.v};
   const int R[2] = {m0.R, m1.R}, J[2] = {m0.J, m1.J}, r[2] = {m0.r, m1.r};
@@ -962,10 +994,14 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (rc) return rc;
   // exact tiles run one wave per frame: the schedule for batches that fill the GPU; the
   // blocked schedules split each frame over many waves and win for a few frames per call
-  const bool pc8 = pc_fits(p, L, frames), head = pc_head_fits(p, L, frames), pc4 = pc4_fits(p, L, frames);
-  if ((p->path == 4 || p->path == 5) && !pc8 && !head && !pc4)
-    return fail(ZFFT_EUNSUPPORTED, "PC decimator needs zoom >= 4 (paths 4, 5), frames of >= 16384 "
-                                   "samples and <= 65535 frames per call");
+  const bool pc8 = pc_fits(p, L, frames), head = pc_head_fits(p, L, frames), pc4 = pc4_fits(p, L, frames),
+             pc2 = pc2_fits(p, L, frames);
+  if ((p->path == 4 || p->path == 5) && !pc8 && !head && !pc4 && !pc2)
+    return fail(ZFFT_EUNSUPPORTED, "PC decimator needs frames of >= 16384 samples and <= 65535 "
+                                   "frames per call");
+  // zoom 2: the tiles on request (paths 4, 5) and automatic below 512 frames per call
+  if (pc2 && (p->path == 4 || p->path == 5 || (p->path == 0 && frames < kPc2TilesMaxFrames)))
+    return run_pc(p, in, L, frames, n, false, out, st, 1);
   // zoom 4: the walk on request, the tiles on request and automatic below 1024 frames per call
   if (pc4 && (p->path == 4 || p->path == 5 || (p->path == 0 && frames < kPc4TilesMaxFrames)))
     return run_pc(p, in, L, frames, n, p->path == 5, out, st, p->K);
@@ -1259,7 +1295,7 @@ int zfft_plan_destroy(zfft_plan *p) {
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->in2, &p->yf, &p->ping, &p->pong, &p->rows,
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
                     &p->tws, &p->means, &p->z4, &p->winf, &p->pc_tab, &p->pc_edge, &p->pc_tab4,
-                    &p->wparts, &p->lo1, &p->lut_d, &p->rgba, &p->al_hist, &p->al_bins})
+                    &p->wparts, &p->lo1, &p->pc_tab2, &p->lut_d, &p->rgba, &p->al_hist, &p->al_bins})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->done_ev) (void)hipEventDestroy(p->done_ev);
@@ -1402,7 +1438,8 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
     B = (frames + nb - 1) / nb;
     const int need = L <= kXaShortFrame ? kXaMinFramesShort : kXaMinFrames;
     if (p->path == 0 && p->K > 0 && !pc_fits(p, L, frames) &&
-        !(pc4_fits(p, L, frames) && frames < kPc4TilesMaxFrames) && auto_xa(frames, L) && B < need) {
+        !(pc4_fits(p, L, frames) && frames < kPc4TilesMaxFrames) &&
+        !(pc2_fits(p, L, frames) && frames < kPc2TilesMaxFrames) && auto_xa(frames, L) && B < need) {
       nb = std::max(1, frames / need);
       B = (frames + nb - 1) / nb;
     }

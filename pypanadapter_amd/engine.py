@@ -122,7 +122,8 @@ class ZoomFFT:
         cascade tiles (zoom 8, frames >= 16384 samples; the auto choice there below 4096
         frames per call), 5 the PC walk (one workgroup per frame; zoom 8: auto from 4096
         frames; zoom 4: the two-stage walk, on request only -- XA is faster there; path 4 at
-        zoom 4 is its tiles, automatic below 1024 frames per call).  At zoom
+        zoom 4 is its tiles, automatic below 1024 frames per call; at zoom 2, 4 and 5 are
+        one-stage tiles in XA's factorisation, automatic below 512).  At zoom
         >= 16, 4 / 5 run PC for the first three stages and XA for the rest; automatic wherever
         XA would take the batch."""
         check(self.lib.zfft_plan_path(self._plan, int(path)), "zfft_plan_path")

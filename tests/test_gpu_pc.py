@@ -154,13 +154,8 @@ def test_pc_matches_xa_and_exact_rows(oracle_lib):
 
 @PC_PATHS
 def test_pc_refuses_outside_its_domain(path):
+    """PC needs frames of >= 16384 samples at every zoom it covers (2 and up)."""
     from pypanadapter_amd import ZoomFFT
-    x = np.zeros(299008, np.complex64)
-    for zoom in (2,):  # zoom 2 has no PC form
-        with ZoomFFT(4096, zoom, 2.4e6) as plan:
-            plan.set_path(path)
-            with pytest.raises(NotImplementedError):
-                plan.rows(x)
     with ZoomFFT(1024, 8, 2.4e6) as plan:
         plan.set_path(path)
         with pytest.raises(NotImplementedError):
@@ -280,6 +275,105 @@ def test_pc_head_auto_batch_rows(oracle_lib):
     assert names[0] == "pc_fir" and "xa_stage" in names and "pc_edge" in names, names
     for f in (0, 191, F - 1):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, 16, 128), f"frame {f}")
+
+
+# ---- zoom 2: the tail kernel on the mixed input (pc_tail_kernel<2>; paths 4 / 5) ----
+
+PC2_LENGTHS = [16384, 16385, 2048 * 9 + 3, 4096 * 4 + 17, 262144, 262144 + 1, 299008 + 3]
+
+
+@pytest.mark.parametrize("flip", [False, True], ids=["noflip", "flip"])
+def test_pc2_decimate_vs_oracle(oracle_lib, flip):
+    """Zoom 2 -- the UI's default fft_ratio (S:1497), one decimate(x, 2) (S:2096-2098) -- at
+    both L mod 2 and across the tile geometry (2048 outputs from a 5376-sample span), against
+    the float64 oracle."""
+    from pypanadapter_amd import ZoomFFT
+    rng = np.random.default_rng(4900 + flip)
+    for L in PC2_LENGTHS:
+        x = (rng.standard_normal(L) + 1j * rng.standard_normal(L)).astype(np.complex64)
+        x += np.exp(2j * np.pi * 0.031 * np.arange(L)).astype(np.complex64)
+        with ZoomFFT(2048, 2, 2.4e6, flip=flip) as plan:
+            plan.set_path(4)
+            plan.set_timing(True)
+            d = plan.decimate(x)
+            names = plan.launch_names()
+        assert names[-1] == "pc_edge", names  # (decimate marks no start: its first launch is unnamed)
+        ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 2, 2.4e6)
+        assert d.shape == ref.shape, (L, d.shape, ref.shape)
+        err = np.abs(d - ref) / np.abs(ref).max()
+        assert err.max() < PC_TOL, (L, flip, float(err.max()), int(err.argmax()), len(d))
+
+
+@pytest.mark.parametrize("N,L,F", [(2048, 262144, 4), (4096, 299008, 3), (1024, 65536 + 1, 5)])
+def test_pc2_rows_vs_oracle(oracle_lib, N, L, F):
+    from pypanadapter_amd import ZoomFFT
+    W = N // 2
+    x = _frames(F, L, N, 2, W, seed0=8700 + N // 1024)
+    with ZoomFFT(N, 2, 2.4e6, n_win=W) as plan:
+        plan.set_path(5)  # (the same tiles as path 4: zoom 2 has no walk)
+        rows = plan.rows(x)
+    for f in range(F):
+        assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, 2, W), f"N={N} L={L} frame {f}")
+
+
+def test_pc2_golden_rows():
+    """Every zoom-2 golden row the reference recorded whose frame PC takes (>= 16384)."""
+    from pypanadapter_amd import ZoomFFT
+    from conftest import window_of
+    n = 0
+    for c in golden_cases()["cases"]:
+        if c["zoom"] != 2 or c["n_samples"] < 16384:
+            continue
+        x = case_input(c)
+        with ZoomFFT(c["n_fft"], 2, c["fs"], n_win=c["n_win"], window=window_of(c["window"]),
+                     f_lo=c["f_lo"]) as plan:
+            plan.set_path(4)
+            row = plan.rows(x)
+        assert_row_close(row, golden_rows()[c["name"]], c["name"])
+        n += 1
+    assert n >= 1
+
+
+@pytest.mark.parametrize("fmt", ["complex32", "cu8", "f32"])
+def test_pc2_input_formats_and_lo(oracle_lib, fmt):
+    """Raw-source formats, np.flip and per-frame LOs read straight into zoom 2's tail kernel."""
+    from pypanadapter_amd import ZoomFFT
+    F, L, N = 3, 131072 + 1, 2048
+    f_lo = [1.0, 150e3 + 1.0, -300e3 + 1.0]
+    x = np.stack([_frames(1, L, N, 2, 1024, seed0=8900 + f, f_lo=f_lo[f])[0] for f in range(F)])
+    arr, vals = _encode(x, fmt)
+    with ZoomFFT(N, 2, 2.4e6, n_win=1024, in_dtype=fmt, flip=True) as plan:
+        plan.set_path(4)
+        plan.set_lo_frames(f_lo, 1)
+        rows = plan.rows(arr)
+    for f in range(F):
+        assert_row_close(rows[f], oracle_lib.psd_row(vals[f, ::-1], 2.4e6, N, 2, 1024, f_lo=f_lo[f]),
+                         f"{fmt} frame {f}")
+
+
+def test_pc2_size_independent_properties():
+    """Determinism, frame-order equivariance, exact x2 scaling, and the tiles against the XA
+    schedule on the same batch."""
+    from pypanadapter_amd import ZoomFFT
+    x = _frames(8, 262144, 2048, 2, 1024, seed0=9100)
+    with ZoomFFT(2048, 2, 2.4e6) as plan:
+        plan.set_path(4)
+        plan.set_timing(True)
+        a = plan.rows(x)
+        assert plan.launch_names()[:2] == ["pc_tail", "pc_edge"], plan.launch_names()
+        b = plan.rows(x)
+        perm = np.random.default_rng(3).permutation(8)
+        c = plan.rows(x[perm])
+        d = plan.rows(2 * x)
+        da = plan.decimate(x[5])
+        plan.set_path(3)
+        xa = plan.rows(x)
+        dx = plan.decimate(x[5])
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(c, a[perm])
+    np.testing.assert_allclose(d - a, 20 * np.log10(4.0), atol=2e-4)
+    assert np.abs(da - dx).max() / np.abs(dx).max() < 2 * PC_TOL
+    np.testing.assert_allclose(xa, a, atol=2e-3)
 
 
 # ---- zoom 4: the tiles (path 4; automatic below XA's batch) and the walk (path 5) ----

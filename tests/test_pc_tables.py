@@ -226,3 +226,88 @@ def test_pc4_model_plus_edge_maps_is_reference_decimate(L):
     out[len(out) - CR.shape[0]:] += (CR @ x[::-1][:CR.shape[1]])[::-1]
     err = np.abs(out - ref).max() / np.abs(ref).max()
     assert err < 2e-7, err
+
+
+# ---- zoom 2 (one stage; PcTab2, pc_tail_kernel<2>: XA's factorisation as tiles) ----
+
+def _model2():
+    """v = x / D(z) (4 sections, causal), u = (M * v)|2 with M = N(z) N(1/z) D(-1/z) as the
+    powers z^-8 .. z^16, out = u / D2(1/w) (4 sections, anticausal), sections slowest first."""
+    s = _secs()
+    n9 = SOS[0, 0] * np.array([1, 8, 28, 56, 70, 56, 28, 8, 1.0])
+    dneg = _neg(_poly(*s[0], range(4)))           # D(-z): coefficient k of z^-k
+    # Laurent product, as {power: coefficient}
+    terms = {}
+    for k, a in enumerate(n9):                      # N(z): z^-k
+        for j, b in enumerate(n9):                  # N(1/z): z^+j
+            for q, c in enumerate(dneg):            # D(-1/z): z^+q
+                p = -k + j + q
+                terms[p] = terms.get(p, 0.0) + a * b * c
+    M = np.array([terms[p] for p in range(-8, 17)])
+    own = sorted([(s[0][0][i], s[0][1][i]) for i in range(4)], key=lambda p: -p[1])
+    ap = sorted([(s[1][0][i], s[1][1][i]) for i in range(4)], key=lambda p: -p[1])
+    return M, own, ap
+
+
+def _edge2(side, lm, shipped=False):
+    if shipped:
+        v = _call(17, 0 if side == 0 else 1 + lm)
+        R, J, r = int(v[0]), int(v[1]), int(v[2])
+        return v[3:3 + R * r].reshape(R, r), v[3 + R * r:3 + R * r + J * r].reshape(r, J).T
+    v = _call(15 + side, lm)
+    R, J, r = int(v[0]), int(v[1]), int(v[2])
+    return v[3:3 + R * r].reshape(R, r), v[3 + R * r:3 + R * r + J * r].reshape(J, r)
+
+
+def test_pc2_taps_and_sections():
+    """Zoom 2's FIR is M = N(z) N(1/z) D(-1/z) (25 taps, z^-8 first), its input-rate sections
+    the stage's four and its output-rate sections those squared (D2), slowest first."""
+    M, own, ap = _model2()
+    v = _call(6)
+    assert v.size == 25 + 8 + 8
+    np.testing.assert_allclose(v[:25], M, rtol=0, atol=6e-8 * np.abs(M).max())  # fp32 taps
+    np.testing.assert_allclose(v[25:33].reshape(4, 2), np.array(own), rtol=1e-7)
+    np.testing.assert_allclose(v[33:].reshape(4, 2), np.array(ap), rtol=1e-7)
+
+
+@pytest.mark.parametrize("side,lm", [(0, 0), (1, 0), (1, 1)])
+def test_pc2_shipped_edge_maps_are_the_builders(side, lm):
+    Ub, Vb = _edge2(side, lm)
+    Us, Vs = _edge2(side, lm, shipped=True)
+    assert Ub.shape == Us.shape and Vb.shape == Vs.shape
+    np.testing.assert_array_equal(Us, Ub)
+    np.testing.assert_array_equal(Vs, Vb)
+
+
+@pytest.mark.parametrize("L", [16384, 16385, 20006, 262144 + 1])
+def test_pc2_model_plus_edge_maps_is_reference_decimate(L):
+    """Zoom 2 (the UI's default fft_ratio, S:1497): the one-stage model -- D forward at the
+    input rate, M, D2 backward at half rate -- and its shipped frame-end maps give scipy's
+    decimate(x, 2) for both L mod 2."""
+    M, own, ap = _model2()
+    rng = np.random.default_rng(L + 2)
+    x = rng.standard_normal(L) + 1j * rng.standard_normal(L)
+    x += 3 * np.exp(2j * np.pi * 0.041 * np.arange(L))
+    ref = ss.decimate(x, 2)
+    pad = 4096
+    y = np.concatenate([np.zeros(pad), x, np.zeros(pad)])
+    so = np.array([[1, 0, 0, 1, a1, a2] for a1, a2 in own])
+    v = ss.sosfilt(so, y)
+    m = np.arange(len(y) // 2)
+    u = np.zeros(len(m), complex)
+    for i, c in enumerate(M):                  # u[m] = sum_p M_p v[2 m + p], p = i - 8
+        idx = 2 * m + i - 8
+        ok = (idx >= 0) & (idx < len(v))
+        u[ok] += c * v[idx[ok]]
+    sa = np.array([[1, 0, 0, 1, a1, a2] for a1, a2 in ap])
+    out = ss.sosfilt(sa, u[::-1])[::-1][pad // 2:pad // 2 + (L + 1) // 2]
+    assert out.shape == ref.shape
+    inner = np.abs(out - ref)[300:-300].max() / np.abs(ref).max()
+    assert inner < 1e-12, inner
+    UL, VL = _edge2(0, L % 2, shipped=True)
+    UR, VR = _edge2(1, L % 2, shipped=True)
+    CL, CR = UL @ VL.T, UR @ VR.T
+    out[:CL.shape[0]] += CL @ x[:CL.shape[1]]
+    out[len(out) - CR.shape[0]:] += (CR @ x[::-1][:CR.shape[1]])[::-1]
+    err = np.abs(out - ref).max() / np.abs(ref).max()
+    assert err < 2e-7, err
