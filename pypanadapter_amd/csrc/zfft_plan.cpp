@@ -955,10 +955,11 @@ int run_pc_head(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std
   const int64_t n3 = n[kPcStages];
   const bool xa_tail = auto_xa(frames, n3);
   hipError_t e = hipSuccess;
-  if (!xa_tail) {  // pong must not move under the head's output when the blocked passes size it
+  if (!xa_tail) {  // ping / pong must not move under a stage's input once the tail sizes them
     const size_t G = (size_t)(frames + 63) / 64 * 64;
     e = p->pong.ensure(std::max((size_t)frames * n3, p->K > kPcStages + 1 ? G * n[kPcStages + 2] : 0) *
                        sizeof(float2));
+    if (e == hipSuccess) e = p->ping.ensure(G * n[kPcStages + 1] * sizeof(float2));
     if (e == hipSuccess && p->lo1.cap < (size_t)n3 * sizeof(float2)) {
       e = p->lo1.ensure((size_t)n3 * sizeof(float2));
       if (e == hipSuccess) e = launch_fill_c64(p->lo1.as<float2>(), n3, 1.f, 0.f, st);
@@ -968,8 +969,31 @@ int run_pc_head(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std
   int rc = run_pc(p, in, L, frames, n, walk, &cur, st, kPcStages);
   if (rc) return rc;
   if (!xa_tail) {
-    const InDesc src{cur, n3, n3, kInC64, 0};
-    return run_exact(p, src, p->lo1.as<float2>(), frames, n, out, st, 0, 0, kPcStages);
+    // zoom 2's tiles (XA's factorisation, the unit LO table) while a stage's input has >= 16384
+    // samples, ping, pong, ... in turn; the blocked passes for the stages after that
+    int k = kPcStages;
+    for (; k < p->K && n[k] >= kPcMinL; ++k) {
+      float2 *dst = ((k - kPcStages) & 1) ? p->pong.as<float2>() : p->ping.as<float2>();
+      const InDesc src{cur, n[k], n[k], kInC64, 0};
+      e = launch_pc2_tail(src, p->lo1.as<float2>(), dst, n[k + 1], frames, p->pc_tab2.as<PcTab2>(), st);
+      if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
+      mark(p, st, "pc_tail");
+      const float *eb = p->pc_edge.as<float>();
+      const PcEdgeConst &m0 = kPcEdge2Idx[0], &m1 = kPcEdge2Idx[1 + (n[k] & 1)];
+      const float *const U[2] = {eb + m0.u, eb + m1.u};
+      const float *const V[2] = {eb + m0.v, eb + m1.v};
+      const int R[2] = {m0.R, m1.R}, J[2] = {m0.J, m1.J}, r[2] = {m0.r, m1.r};
+      e = launch_pc_edge(src, p->lo1.as<float2>(), dst, n[k + 1], frames, U, V, R, J, r, st);
+      if (e != hipSuccess) return hip_fail(e, "pc_edge launch");
+      mark(p, st, "pc_edge");
+      cur = dst;
+    }
+    if (k == p->K) {
+      *out = cur;
+      return ZFFT_OK;
+    }
+    const InDesc src{cur, n[k], n[k], kInC64, 0};
+    return run_exact(p, src, p->lo1.as<float2>(), frames, n, out, st, 0, 0, k);
   }
   e = p->ping.ensure((size_t)frames * n[kPcStages + 1] * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");

@@ -222,8 +222,9 @@ def test_pc_ragged_lengths_on_a_caller_stream(oracle_lib, zfft_lib, path):
 @PC_PATHS
 def test_pc_head_decimate_vs_oracle(oracle_lib, zoom, flip, path):
     """decimate(x, 2) x log2(zoom) as PC's exact x8 (frame-end maps at every L mod 8) followed,
-    for one frame per call, by the exact blocked passes on its output (a unit LO table), against
-    the float64 oracle; 1e-5 per tail stage on top."""
+    for one frame per call, by zoom 2's tiles while a stage's input has >= 16384 samples and
+    the exact blocked passes after that (both on a unit LO table), against the float64 oracle;
+    1e-5 per tail stage on top."""
     from pypanadapter_amd import ZoomFFT
     rng = np.random.default_rng(4600 + zoom + flip)
     for L in [16384, 16387, 16390, 3968 * 5 + 1, 262144 + 5, 299008]:
@@ -234,7 +235,14 @@ def test_pc_head_decimate_vs_oracle(oracle_lib, zoom, flip, path):
             plan.set_timing(True)
             d = plan.decimate(x)
             names = plan.launch_names()
-        assert names.count("exact_backward") == {16: 1, 32: 2}[zoom], names  # one frame: blocked tail
+        # one frame: zoom 2's tiles for the tail stages whose input has >= 16384 samples,
+        # then the blocked passes
+        n = [L]
+        while len(n) <= {16: 4, 32: 5}[zoom]:
+            n.append((n[-1] + 1) // 2)
+        tiles = next((k - 3 for k in range(3, len(n) - 1) if n[k] < 16384), len(n) - 4)
+        assert names.count("exact_backward") == len(n) - 4 - tiles, (L, names)
+        assert names.count("pc_tail") == tiles + (path == 4), (L, names)
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, zoom, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
         err = np.abs(d - ref) / np.abs(ref).max()
