@@ -953,7 +953,8 @@ int run_pc_head(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std
                 bool walk, const float2 **out, hipStream_t st) {
   const float2 *cur = nullptr;
   const int64_t n3 = n[kPcStages];
-  const bool xa_tail = auto_xa(frames, n3);
+  // XA where it takes the batch, except where zoom 2's tiles still beat it (< 512 frames)
+  const bool xa_tail = auto_xa(frames, n3) && !(frames < kPc2TilesMaxFrames && n3 >= kPcMinL);
   hipError_t e = hipSuccess;
   if (!xa_tail) {  // ping / pong must not move under a stage's input once the tail sizes them
     const size_t G = (size_t)(frames + 63) / 64 * 64;

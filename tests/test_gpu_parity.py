@@ -430,14 +430,16 @@ def test_facade_matches_reference_rows():
                                         (4, 1023, 65536, "pc"), (4, 1024, 65536, "xa"),
                                         (2, 512, 65536, "xa"), (2, 511, 65536, "pc2"), (2, 8, 262144, "pc2"),
                                         (2, 8, 8192, "exact"),
-                                        (16, 384, 262144, "pc"), (16, 8, 262144, "pc")])
+                                        (16, 384, 262144, "pc"), (16, 512, 262144, "pc"),
+                                        (16, 8, 262144, "pc")])
 def test_auto_schedule_by_batch(z, F, L, want):
     """The automatic decimator schedule follows the measured crossovers (zfft_plan.cpp
     pc_fits / kPcWalkMinFrames / auto_xa / use_fused, tools/sweep_schedule.py,
     profiles/r04l): at zoom 8 the PC polyphase cascade for every batch of frames >= 16384
     samples (one frame per call -- the reference's use -- included), as its walk kernel
     from 4096 frames per call; zoom >= 16 as PC's first three stages + XA where XA would take
-    the batch (zoom 2's tiles on the 1/8-rate output below that); PC's tiles at zoom 4
+    the batch and zoom 2's tiles does not (>= 512 frames; zoom 2's tiles below that, then the
+    blocked passes under 16384 samples); PC's tiles at zoom 4
     below 1024 frames per call and at zoom 2 below 512, XA from there; for frames < 16384 samples
     >= 384 frames of <= 2^19 samples (768 of longer ones) the XA tiles and smaller batches the
     exact blocked passes (the fused interior with edge windows is reached on request only)."""
@@ -457,8 +459,8 @@ def test_auto_schedule_by_batch(z, F, L, want):
              "xa": ("xa_stage_mix",), "pc": ("pc_fir",), "pc2": ("pc_tail",), "walk": ("pc_walk",)}[want]
     assert names[0] in first, names
     assert ("edge_windows" in names) == (want == "fused"), names
-    if z == 16:  # the PC head's tail stage: XA's where XA takes the batch, else zoom 2's tiles
-        assert ("xa_stage" in names) == (F >= 384) and names.count("pc_edge") == (1 if F >= 384 else 2), names
+    if z == 16:  # the PC head's tail stage: zoom 2's tiles below 512 frames, else XA's
+        assert ("xa_stage" in names) == (F >= 512) and names.count("pc_edge") == (1 if F >= 512 else 2), names
     del x, rows
     torch.cuda.empty_cache()
 

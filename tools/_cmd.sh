@@ -3,4 +3,4 @@
 # trace, PMC traffic and SQ counters (stamped into profiles/), every BASELINE config.
 set -u
 export TMPDIR=/tmp
-bash tools/gpu_session.sh r05fin5 tests smoke driver prof pmc sq stamp cfgs
+bash tools/gpu_session.sh r05fin6 tests smoke driver prof pmc sq stamp cfgs
