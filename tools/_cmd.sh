@@ -1,6 +1,5 @@
 # Scratch GPU command of the current session (run as: gpurun -- 'bash tools/_cmd.sh'):
-# the final-sources session: GPU tests, smoke, the driver's bench line, rocprofv3 kernel
-# trace, PMC traffic and SQ counters (stamped into profiles/), every BASELINE config.
+# cfg5 PMC traffic (complex64, complex32) at the final sources, and the schedule sweep.
 set -u
 export TMPDIR=/tmp
-bash tools/gpu_session.sh r05fin6 tests smoke driver prof pmc sq stamp cfgs
+bash tools/gpu_session.sh r05fin6b pmc5
