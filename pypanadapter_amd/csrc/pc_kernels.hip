@@ -68,6 +68,15 @@ constexpr int kKo = 0;
 #ifndef PC_OCC3
 #define PC_OCC3 0
 #endif
+// PC_CENSUS (diagnostic builds only, listing only, wrong at frame edges): every walk sub-tile
+// takes the interior path, so the edge code is dead and the assembly is the steady-state tile
+// that tools/isa_census.py counts
+#if !ZFFT_DIAG && defined(PC_CENSUS)
+#error "PC_CENSUS is a diagnostic knob: build with -DZFFT_DIAG"
+#endif
+#ifndef PC_CENSUS
+#define PC_CENSUS 0
+#endif
 
 namespace zfft {
 namespace pc {
@@ -409,8 +418,10 @@ __device__ __forceinline__ void sec_block(v2f (&v)[B], TP tab0, LP scr, int lane
       e0 = n0;
     }
   }
+  // the lane without a source reads 0 from the shift (bound_ctrl), which is the zero
+  // entering state of a block that does not continue another wave
   v2f i0 = wshift<UP>(e0), i1 = wshift<UP>(e1);
-  if (lane == (UP ? 0 : 63)) {
+  if (XW && lane == (UP ? 0 : 63)) {
     i0 = s0;
     i1 = s1;
   }
@@ -451,8 +462,7 @@ __device__ __forceinline__ void sec_run(v2f (&v)[B], CS S, int lane) {
     e1 = fma2(&S.pw[d][2], p0, p1, e1);
     e0 = n0;
   }
-  v2f i0 = wshift<UP>(e0), i1 = wshift<UP>(e1);
-  if (lane == (UP ? 0 : 63)) i0 = i1 = splat(0.f);
+  const v2f i0 = wshift<UP>(e0), i1 = wshift<UP>(e1);  // 0 on the first lane (bound_ctrl)
 #pragma unroll
   for (int c = 0; c < DCUT; ++c) {
     const int k = UP ? c : B - 1 - c;
@@ -611,6 +621,10 @@ template <int B, int LEV, bool UP, int SI, class TP>
 __device__ __forceinline__ void wsec(v2f (&v)[B], TP tab0, LP scr, int lane, int wave, v2f c0, v2f c1) {
   const TP tab = fresh(tab0);
   CS S = UP ? tab->wf[SI] : tab->wb[SI];
+  // this lane's cross-wave factors A^(B (dist + 1)), loaded first: the run hides their latency
+  const int dist = UP ? lane : 63 - lane;
+  typedef float v4u __attribute__((ext_vector_type(4), aligned(4)));
+  const v4f xw = *(const v4u __attribute__((address_space(4))) *)(UP ? &tab->wf_x[SI][dist][0] : &tab->wb_x[SI][dist][0]);
   const v2f na1 = splat(-S.a1), na2 = splat(-S.a2);
   v2f y1 = splat(0.f), y2 = splat(0.f);
 #pragma unroll
@@ -646,10 +660,8 @@ __device__ __forceinline__ void wsec(v2f (&v)[B], TP tab0, LP scr, int lane, int
     s1 = scr[2 * src + 1];
   }
   {
-    const int dist = UP ? lane : 63 - lane;
-    const float __attribute__((address_space(4))) *x = UP ? &tab->wf_x[SI][dist][0] : &tab->wb_x[SI][dist][0];
-    const v2f n0 = vfma(splat(x[0]), s0, vfma(splat(x[1]), s1, e0));
-    e1 = vfma(splat(x[2]), s0, vfma(splat(x[3]), s1, e1));
+    const v2f n0 = vfma(splat(xw.x), s0, vfma(splat(xw.y), s1, e0));
+    e1 = vfma(splat(xw.z), s0, vfma(splat(xw.w), s1, e1));
     e0 = n0;
   }
   v2f i0 = wshift<UP>(e0), i1 = wshift<UP>(e1);
@@ -728,7 +740,7 @@ pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, typename WalkZ<ZO
   // sub-tile g's first input sample; inside the frame ("fast") its pairs are prefetched into
   // registers one sub-tile ahead (the first of a tile during the previous tile's sections)
   auto xs_of = [&](int g) { return Z::xs_of(g); };
-  auto fast = [&](int64_t xs) { return xs >= 0 && xs + kPcK1In <= L; };
+  auto fast = [&](int64_t xs) { return PC_CENSUS || (xs >= 0 && xs + kPcK1In <= L); };
   typename RawP<DT>::T pf[9];
   auto prefetch = [&](int g) {
     const int64_t xs = xs_of(g);
@@ -770,7 +782,6 @@ pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, typename WalkZ<ZO
           const v2f cc = lane_val(lo_cur, 8 * c + i);  // lo[xs + 512 i]
           *(LP4)(xl + xidx(s)) = cat(cmul2(a, cmul2(cc, lo2(lane_lo))), cmul2(b, cmul2(cc, hi2(lane_lo))));
         }
-        prefetch(Z::SUB * tau + c + 1);
       } else {
         for (int s = t; s < kPcK1In; s += 256) {
           const int64_t n = xs + s;
@@ -778,8 +789,12 @@ pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, typename WalkZ<ZO
           if (n >= 0 && n < L) v = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
           xl[xidx(s)] = v;
         }
-        prefetch(Z::SUB * tau + c + 1);
       }
+      // one call site for both paths: the loads land in the same registers on either, so the
+      // compiler's wait tracking has no stale load to drain (two call sites made it put a
+      // vmcnt(0) right behind the barrier, exposing every prefetch's round trip); the next
+      // tile's first sub-tile is fetched after the own-rate sections' table loads instead
+      if (c + 1 < Z::SUB) prefetch(Z::SUB * tau + c + 1);
       if constexpr (!(kKo & 64)) __syncthreads();
       PC_STAMP(0);
       v2f acc[8];
@@ -881,6 +896,7 @@ pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, typename WalkZ<ZO
 #pragma unroll
       for (int k = 0; k < kPcWb; ++k) zb[k] = v[k];
     }
+    prefetch(Z::SUB * (tau + 1));  // overlaps FIR gamma, the output-rate sections and the stores
     __syncthreads();
     PC_STAMP(5);
     // ---- FIR gamma (K2's): u3 index k = 9 t + r (output m0 - 128 + k) from z s in [2k + 276, + 56]
