@@ -161,6 +161,15 @@ __device__ __forceinline__ void fir_pair(v2f &acc, TP taps, int u, v2f x0, v2f x
     if (u + 1 >= 0 && u + 1 < G) acc = vfma(splat(taps[u + 1]), x1, acc);
   }
 }
+// cmul2 with a wave-uniform first factor held in an SGPR pair (VOP3P takes it as a source:
+// no v_mov of the pair into VGPRs first)
+__device__ __forceinline__ v2f cmul2s(v2f a, v2f b) {
+  v2f t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "s"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=v"(r) : "s"(a), "v"(b), "v"(t));
+  return r;
+}
 // lane k's v of a wave, for a wave-uniform k (v_readlane: an SGPR pair, no memory round trip)
 __device__ __forceinline__ v2f lane_val(v2f v, int k) {
   return v2f{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), k)),
@@ -780,7 +789,7 @@ pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, typename WalkZ<ZO
           v2f a, b;
           cvt_pair<DT, FLIP>(pf[i], a, b);
           const v2f cc = lane_val(lo_cur, 8 * c + i);  // lo[xs + 512 i]
-          *(LP4)(xl + xidx(s)) = cat(cmul2(a, cmul2(cc, lo2(lane_lo))), cmul2(b, cmul2(cc, hi2(lane_lo))));
+          *(LP4)(xl + xidx(s)) = cat(cmul2(a, cmul2s(cc, lo2(lane_lo))), cmul2(b, cmul2s(cc, hi2(lane_lo))));
         }
       } else {
         for (int s = t; s < kPcK1In; s += 256) {
@@ -1008,6 +1017,57 @@ __global__ void __launch_bounds__(256) pc_edge_kernel(InDesc in, const v2f *lo, 
   }
 }
 
+// K3 split for the walk: KV makes v = V^T x for every frame end on a side
+// stream while the walk runs -- one wave per (frame, side, 4 ranks), no LDS and few VGPRs, so its
+// waves fit beside the walk's two workgroups per CU and use issue slots the walk leaves idle --
+// and KU adds U v to the walk's output once both are done (a tiny launch).  Same sums as K3.
+constexpr int kEdgeRanksPerWave = 4;
+template <int DT, int FLIP>
+__global__ void __launch_bounds__(64) pc_edge_v_kernel(InDesc in, const v2f *lo, v2f *vout,
+                                                       const float *V0, int J0, int r0,
+                                                       const float *V1, int J1, int r1) {
+  const int lane = threadIdx.x;
+  const int64_t f = blockIdx.x, L = in.len;
+  const int side = blockIdx.y, k0 = kEdgeRanksPerWave * blockIdx.z;
+  const float *V = side ? V1 : V0;
+  const int J = side ? J1 : J0, r = side ? r1 : r0;
+  if (k0 >= r) return;  // wave-uniform
+  const v2f *lor = lo_row(lo, in, f);
+  v2f acc[kEdgeRanksPerWave];
+#pragma unroll
+  for (int k = 0; k < kEdgeRanksPerWave; ++k) acc[k] = splat(0.f);
+  for (int j = lane; j < J; j += 64) {
+    const int64_t n = side ? L - 1 - j : j;
+    const v2f x = cmul2(load_in_t<DT, FLIP>(in, f, n), lor[n]);
+#pragma unroll
+    for (int k = 0; k < kEdgeRanksPerWave; ++k)
+      if (k0 + k < r) acc[k] = vfma(splat(V[(int64_t)(k0 + k) * J + j]), x, acc[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kEdgeRanksPerWave; ++k) {
+    v2f a = acc[k];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) a += shxor(a, d);
+    if (lane == 0 && k0 + k < r) vout[(f * 2 + side) * kPcEdgeRank + k0 + k] = a;
+  }
+}
+// out[m] += sum_k U[m][k] v[k] at both ends: one block per frame, thread t < R0 the start's
+// output t, thread 192 + t < 192 + R1 the end's output n3 - 1 - t
+__global__ void __launch_bounds__(384) pc_edge_u_kernel(const v2f *vin, v2f *out, int64_t n3,
+                                                        const float *U0, int R0, int r0,
+                                                        const float *U1, int R1, int r1) {
+  const int side = threadIdx.x >= kPcEdgeR, t = threadIdx.x - (side ? kPcEdgeR : 0);
+  const int R = side ? R1 : R0, r = side ? r1 : r0;
+  if (t >= R) return;
+  const int64_t f = blockIdx.x;
+  const float *U = side ? U1 : U0;
+  const v2f *v = vin + (f * 2 + side) * kPcEdgeRank;
+  v2f c = splat(0.f);
+  for (int k = 0; k < r; ++k) c = vfma(splat(U[t * r + k]), v[k], c);
+  const int64_t m = side ? n3 - 1 - t : t;
+  out[f * n3 + m] += c;
+}
+
 }  // namespace pc
 
 // Debug hook (not part of zfft.h): copies and clears the walk's stamp sums of a PC_STAMPS build
@@ -1121,6 +1181,21 @@ hipError_t launch_pc_walk4(const InDesc &in, const float2 *lo, float2 *out, int6
                            const PcTab4 *tab, hipStream_t st) {
   PC_DISPATCH_Z(pc::pc_walk_kernel, 4, in, dim3((unsigned)frames), dim3(256), 0, st, in, (const v2f *)lo,
                 (v2f *)out, n2, (pc::CT4)tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_pc_edge_v(const InDesc &in, const float2 *lo, float2 *v, int frames,
+                            const float *const V[2], const int J[2], const int r[2], hipStream_t st) {
+  const dim3 grid(frames, 2, (kPcEdgeRank + pc::kEdgeRanksPerWave - 1) / pc::kEdgeRanksPerWave);
+  PC_DISPATCH(pc::pc_edge_v_kernel, in, grid, dim3(64), 0, st, in, (const v2f *)lo, (v2f *)v, V[0], J[0],
+              r[0], V[1], J[1], r[1]);
+  return hipGetLastError();
+}
+
+hipError_t launch_pc_edge_u(const float2 *v, float2 *out, int64_t n3, int frames, const float *const U[2],
+                            const int R[2], const int r[2], hipStream_t st) {
+  hipLaunchKernelGGL(pc::pc_edge_u_kernel, dim3(frames), dim3(2 * kPcEdgeR), 0, st, (const v2f *)v,
+                     (v2f *)out, n3, U[0], R[0], r[0], U[1], R[1], r[1]);
   return hipGetLastError();
 }
 

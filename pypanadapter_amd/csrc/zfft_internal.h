@@ -257,6 +257,12 @@ hipError_t launch_pc_walk(const InDesc &in, const float2 *lo, float2 *out, int64
 hipError_t launch_pc_walk4(const InDesc &in, const float2 *lo, float2 *out, int64_t n2, int frames,
                            const PcTab4 *tab, hipStream_t st);
 // both frame ends in one launch: [0] = start, [1] = end
+// K3 split (the walk): v = V^T x per frame end into v[frames][2][kPcEdgeRank] (may run on a
+// side stream beside the walk), then out += U v
+hipError_t launch_pc_edge_v(const InDesc &in, const float2 *lo, float2 *v, int frames,
+                            const float *const V[2], const int J[2], const int r[2], hipStream_t st);
+hipError_t launch_pc_edge_u(const float2 *v, float2 *out, int64_t n3, int frames, const float *const U[2],
+                            const int R[2], const int r[2], hipStream_t st);
 hipError_t launch_pc_edge(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
                           const float *const U[2], const float *const V[2], const int R[2],
                           const int J[2], const int r[2], hipStream_t st);

@@ -425,6 +425,10 @@ struct zfft_plan {
   hipEvent_t done_ev = nullptr;
   hipStream_t done_st = nullptr;
   bool has_work = false;
+  // the walk's frame-end sums V^T x run on side_st beside it (fork_ev / join_ev), into edge_v
+  hipStream_t side_st = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  DevBuf edge_v;
 };
 
 namespace {
@@ -906,18 +910,24 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
                         p->pc_tab4.as<PcTab4>(), st);
     if (e != hipSuccess) return hip_fail(e, "pc_tail launch");
     mark(p, st, "pc_tail");
-  } else if (K == 2) {  // zoom 4: the walk
+  } else if (walk) {  // one launch, y2 (zoom 4: y1) in LDS; the frame-end sums beside it
     e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
+    if (e == hipSuccess) e = p->edge_v.ensure((size_t)frames * 2 * kPcEdgeRank * sizeof(float2));
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
-    e = launch_pc_walk4(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab4.as<PcTab4>(), st);
-    if (e != hipSuccess) return hip_fail(e, "pc_walk4 launch");
-    mark(p, st, "pc_walk4");
-  } else if (walk) {  // one launch, y2 in LDS
-    e = p->pong.ensure((size_t)frames * n3 * sizeof(float2));
-    if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
-    e = launch_pc_walk(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, tab, st);
+    e = hipEventRecord(p->fork_ev, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(p->side_st, p->fork_ev, 0);
+    if (e != hipSuccess) return hip_fail(e, "side stream fork");
+    if (K == 2) e = launch_pc_walk4(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab4.as<PcTab4>(), st);
+    else e = launch_pc_walk(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, tab, st);
     if (e != hipSuccess) return hip_fail(e, "pc_walk launch");
-    mark(p, st, "pc_walk");
+    mark(p, st, K == 2 ? "pc_walk4" : "pc_walk");
+    const float *eb = p->pc_edge.as<float>();
+    const PcEdgeConst &m0 = K == 2 ? kPcEdge4Idx[0] : kPcEdgeIdx[0];
+    const PcEdgeConst &m1 = K == 2 ? kPcEdge4Idx[1 + (L & 3)] : kPcEdgeIdx[1 + (L & 7)];
+    const float *const V[2] = {eb + m0.v, eb + m1.v};
+    const int J[2] = {m0.J, m1.J}, r[2] = {m0.r, m1.r};
+    e = launch_pc_edge_v(in, p->lo.as<float2>(), p->edge_v.as<float2>(), frames, V, J, r, p->side_st);
+    if (e != hipSuccess) return hip_fail(e, "pc_edge_v launch");
   } else {
     const int64_t y2s = (pc_y2_len(L) + kPcK1Q - 1) / kPcK1Q * kPcK1Q;
     e = p->ping.ensure((size_t)frames * y2s * sizeof(float2));
@@ -939,7 +949,13 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
   const float *const U[2] = {eb + m0.u, eb + m1.u};
   const float *const V[2] = {eb + m0.v, eb + m1.v};
   const int R[2] = {m0.R, m1.R}, J[2] = {m0.J, m1.J}, r[2] = {m0.r, m1.r};
-  e = launch_pc_edge(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, U, V, R, J, r, st);
+  if (walk && K >= 2) {  // V^T x ran on the side stream beside the walk: join, then out += U v
+    e = hipEventRecord(p->join_ev, p->side_st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, p->join_ev, 0);
+    if (e == hipSuccess) e = launch_pc_edge_u(p->edge_v.as<float2>(), p->pong.as<float2>(), n3, frames, U, R, r, st);
+  } else {
+    e = launch_pc_edge(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, U, V, R, J, r, st);
+  }
   if (e != hipSuccess) return hip_fail(e, "pc_edge launch");
   mark(p, st, "pc_edge");
   *out = p->pong.as<float2>();
@@ -1267,7 +1283,10 @@ int zfft_plan_create(const zfft_config *cfg, const float *window_or_null, zfft_p
     p->user_window.assign(window_or_null, window_or_null + c.n_fft);
   e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->copy_st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->side_st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&p->done_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&p->join_ev, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) {
     e = hipEventCreateWithFlags(&p->h2d_ev[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->comp_ev[i], hipEventDisableTiming);
@@ -1320,10 +1339,14 @@ int zfft_plan_destroy(zfft_plan *p) {
   for (DevBuf *b : {&p->lo, &p->win, &p->tw, &p->in, &p->in2, &p->yf, &p->ping, &p->pong, &p->rows,
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
                     &p->tws, &p->means, &p->z4, &p->winf, &p->pc_tab, &p->pc_edge, &p->pc_tab4,
-                    &p->wparts, &p->lo1, &p->pc_tab2, &p->lut_d, &p->rgba, &p->al_hist, &p->al_bins})
+                    &p->wparts, &p->lo1, &p->pc_tab2, &p->lut_d, &p->rgba, &p->al_hist, &p->al_bins,
+                    &p->edge_v})
     b->release();
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->done_ev) (void)hipEventDestroy(p->done_ev);
+  if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
+  if (p->join_ev) (void)hipEventDestroy(p->join_ev);
+  if (p->side_st) (void)hipStreamSynchronize(p->side_st), (void)hipStreamDestroy(p->side_st);
   for (int i = 0; i < 2; ++i) {
     if (p->h2d_ev[i]) (void)hipEventDestroy(p->h2d_ev[i]);
     if (p->comp_ev[i]) (void)hipEventDestroy(p->comp_ev[i]);
