@@ -350,7 +350,10 @@ def display_timing(dev, widths=(512, 8192), lines=12) -> dict:
     D2H, what pyqtgraph's setImage turns the image into, S:1664) or `img_array` (the float64
     image materialised on the host every line, the pre-r04 INTEGRATION.md binding); beside
     them the reference's own `Waterfall.image_update` (oracle/scipy_path.py: full-image
-    np.roll per line, S:1638-1664) on the CPU."""
+    np.roll per line, S:1638-1664) on the CPU.  Since round 6 the facade's image_update
+    stages the row on the host and the next read pushes it (zfft_waterfall_push_render /
+    _push_read64: one kernel, one copy, one wait per line), so "push" alone is host work and
+    the device push is inside the other two columns."""
     import numpy as np
     from oracle.scipy_path import Waterfall as RefWaterfall
     from pypanadapter_amd import Waterfall
@@ -370,7 +373,7 @@ def display_timing(dev, widths=(512, 8192), lines=12) -> dict:
                     wf.render()
                 elif what == "push_img_array":
                     _ = wf.img_array
-                # "push" alone: zfft_waterfall_push synchronises its stream before returning
+                # "push" alone: the facade stages the row (the next read pushes it)
                 if k >= 2:
                     ts.append((time.perf_counter() - t0) * 1e3)
             res[what + "_ms_per_line"] = round(float(np.median(ts)), 3)

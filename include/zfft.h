@@ -174,6 +174,16 @@ int zfft_waterfall_autolevel(zfft_plan *plan, double *minlev, double *maxlev);
 int zfft_waterfall_render(zfft_plan *plan, uint8_t *rgba_out /* host, H*n_win*4 */);
 int zfft_waterfall_render_device(zfft_plan *plan, uint8_t *d_rgba /* H*n_win*4 */,
                                  void *hip_stream);
+/* The per-line display in one round trip (Waterfall.image_update then the image the Qt side
+ * draws, S:1638-1664): `count` host rows of n_win floats pushed as zfft_waterfall_push would
+ * (0 = none), then the image emitted -- RGBA8 as zfft_waterfall_render, or float64 as the
+ * reference's img_array (zfft_waterfall_read's floats widened) -- and copied to the host, with
+ * one kernel for a single row, one copy and one wait (the rows are staged in page-locked
+ * memory the kernel reads in place).  Same ring and image as the separate calls. */
+int zfft_waterfall_push_render(zfft_plan *plan, const float *rows, int32_t count,
+                               uint8_t *rgba_out /* host, H*n_win*4 */);
+int zfft_waterfall_push_read64(zfft_plan *plan, const float *rows, int32_t count,
+                               double *img_out /* host, H*n_win */);
 
 /* Page-locked host memory (hipHostMalloc on the current device), e.g. for rgba_out: a render
  * (or a zfft_process row block) copied into it moves at PCIe DMA rate; into pageable memory

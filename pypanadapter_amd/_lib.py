@@ -61,7 +61,8 @@ EXPORTS = [
     "zfft_ring_state", "zfft_ring_take", "zfft_ring_process",
     "zfft_colormap_lut", "zfft_waterfall_colormap", "zfft_waterfall_levels",
     "zfft_waterfall_get_levels", "zfft_waterfall_autolevel", "zfft_waterfall_render",
-    "zfft_waterfall_render_device", "zfft_host_alloc", "zfft_host_free",
+    "zfft_waterfall_render_device", "zfft_waterfall_push_render", "zfft_waterfall_push_read64",
+    "zfft_host_alloc", "zfft_host_free",
     "zfft_device_count", "zfft_version",
 ]
 
@@ -143,6 +144,8 @@ def load(path: str = ""):
         "zfft_waterfall_autolevel": (ctypes.c_int, [P, ctypes.POINTER(D), ctypes.POINTER(D)]),
         "zfft_waterfall_render": (ctypes.c_int, [P, P]),
         "zfft_waterfall_render_device": (ctypes.c_int, [P, P, P]),
+        "zfft_waterfall_push_render": (ctypes.c_int, [P, P, I32, P]),
+        "zfft_waterfall_push_read64": (ctypes.c_int, [P, P, I32, P]),
         "zfft_host_alloc": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(P)]),
         "zfft_host_free": (ctypes.c_int, [P]),
         "zfft_device_count": (ctypes.c_int, []),

@@ -305,6 +305,11 @@ hipError_t launch_waterfall_push(float *ring, int H, int W, const float *rows,
 hipError_t launch_waterfall_read(const float *ring, int H, int W, int64_t off, float *img,
                                  hipStream_t st);
 // waterfall rendering: RGBA8 pixels of the ring in read order
+// one row (host-visible `row`, or null: none) pushed and the image emitted in one launch:
+// RGBA8 through `lut` (f64 false) or float64 (f64 true) into `out` (H*W pixels)
+hipError_t launch_waterfall_push_emit(float *ring, int H, int W, int64_t off0, int scroll,
+                                      const float *row, const void *lut, double lo, double scale,
+                                      void *out, bool f64, hipStream_t st);
 hipError_t launch_waterfall_render(const float *ring, int H, int W, int64_t off, const void *lut,
                                    double lo, double scale, void *out, hipStream_t st);
 // autolevel order statistics of the pixels < 0: top-16-bit key histogram (65536 bins), then

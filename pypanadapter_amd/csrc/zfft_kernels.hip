@@ -1367,6 +1367,56 @@ __global__ void waterfall_read_kernel(const float *__restrict__ ring, int H, int
   img[i] = ring[(int64_t)((r + off) % H) * W + xcol];
 }
 
+// Per-line display in one launch: push one row (or none) and emit the
+// image -- RGBA8 (MODE 0, as waterfall_render_kernel) or float64 (MODE 1, img_array's dtype).
+// Image row r is ring slot s = (r + off1) mod H after the push (off1 = off0 + scroll).  The
+// row lands in slot (H - 1 + off0) mod H with its grid zeros (waterfall_rows_kernel, r = 0),
+// and this push's tick stamps hit slots (yrow + off1) mod H, i.e. image rows yrow
+// (waterfall_stamps_kernel with count 1: no later push rewrites them).  Pixels and slots are
+// a bijection, so the thread of a changed slot writes it back to the ring unraced.
+template <int MODE>
+__global__ void waterfall_push_emit_kernel(float *__restrict__ ring, int H, int W, int off0, int scroll,
+                                           const float *__restrict__ row, const uchar4 *__restrict__ lut,
+                                           double lo, double scale, void *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)H * W) return;
+  const int r = (int)(i / W), xcol = (int)(i % W);
+  const int off1 = row ? pmod((int64_t)off0 + scroll, H) : off0;
+  const int64_t at = (int64_t)((r + off1) % H) * W + xcol;
+  float v;
+  if (row) {
+    bool dirty = false;
+    if ((r + off1) % H == pmod((int64_t)H - 1 + off0, H)) {
+      v = row[xcol];
+      if (xcol == 0 || xcol == (W >> 1) || xcol == W - 1) v = 0.f;  // grid, S:1646-1648
+      dirty = true;
+    } else {
+      v = ring[at];
+    }
+    const int tick = W / 10;
+    if (tick > 0 && xcol % tick == 0) {  // S:1650-1662
+      const int it = xcol / tick, nt = (W - 1 + tick - 1) / tick;
+      const int y0 = scroll > 0 ? 5 : H - 10, nrows = scroll > 0 ? 10 : 8;
+      if (it < nt && it != 5 && it != 10 && pmod((int64_t)r - y0, H) < nrows) {
+        v = 0.f;
+        dirty = true;
+      }
+    }
+    if (dirty) ring[at] = v;
+  } else {
+    v = ring[at];
+  }
+  if constexpr (MODE == 0) {
+    double t = ((double)v - lo) * scale;
+    t = t < 0.0 ? 0.0 : (t > 255.0 ? 255.0 : t);
+    uchar4 c = lut[v == v ? (int)t : 0];
+    if (v != v) c.w = 0;
+    ((uchar4 *)out)[i] = c;
+  } else {
+    ((double *)out)[i] = (double)v;
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 static inline unsigned nblocks(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
@@ -1626,6 +1676,19 @@ hipError_t launch_waterfall_render(const float *ring, int H, int W, int64_t off,
   const int64_t total = (int64_t)H * W;
   hipLaunchKernelGGL(waterfall_render_kernel, dim3(nblocks(total, 256)), dim3(256), 0, st, ring, H,
                      W, (int)off, (const uchar4 *)lut, lo, scale, (uchar4 *)out);
+  return hipGetLastError();
+}
+
+hipError_t launch_waterfall_push_emit(float *ring, int H, int W, int64_t off0, int scroll,
+                                      const float *row, const void *lut, double lo, double scale,
+                                      void *out, bool f64, hipStream_t st) {
+  const dim3 g(nblocks((int64_t)H * W, 256));
+  if (f64)
+    hipLaunchKernelGGL(waterfall_push_emit_kernel<1>, g, dim3(256), 0, st, ring, H, W, (int)(off0 % H), scroll,
+                       row, (const uchar4 *)lut, lo, scale, out);
+  else
+    hipLaunchKernelGGL(waterfall_push_emit_kernel<0>, g, dim3(256), 0, st, ring, H, W, (int)(off0 % H), scroll,
+                       row, (const uchar4 *)lut, lo, scale, out);
   return hipGetLastError();
 }
 

@@ -409,6 +409,7 @@ struct zfft_plan {
   DevBuf pc_tab2;  // PC zoom 2: PcTab2
   DevBuf wparts;   // split DIF Welch: partial PSDs (frames x split x n_win floats)
   DevBuf lo1;      // unit LO table (the blocked passes after the PC head mix with it)
+  int64_t lo1_n = 0;  // entries of lo1 filled (a failed fill leaves it short: refilled next call)
                            // (pc_edge: all nine maps of pc_edge_maps.h, uploaded once)
   int64_t n_quiesce = 0;   // host waits on enqueued work (test hook zfft__plan_quiesce_count)
   // waterfall rendering: colormap LUT (host copy + device), levels
@@ -418,6 +419,9 @@ struct zfft_plan {
   std::string cmap = "Default";
   double lev_lo = -220.0, lev_hi = -120.0;  // Waterfall.__init__ (S:1593-1598)
   DevBuf lut_d, rgba, al_hist, al_bins;
+  DevBuf img64;                    // float64 image of the display entries
+  float *row_pin = nullptr;        // page-locked staging of host rows the display kernels read
+  size_t row_pin_cap = 0;          //   in place (no H2D copy command); bytes
   // Ordering across streams: every call that enqueues work first makes its stream wait for
   // the plan's previous work (done_ev, recorded on done_st), then records done_ev after its
   // own; the workspaces, tables and the ring are thus used in call order whatever streams the
@@ -977,9 +981,10 @@ int run_pc_head(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std
     e = p->pong.ensure(std::max((size_t)frames * n3, p->K > kPcStages + 1 ? G * n[kPcStages + 2] : 0) *
                        sizeof(float2));
     if (e == hipSuccess) e = p->ping.ensure(G * n[kPcStages + 1] * sizeof(float2));
-    if (e == hipSuccess && p->lo1.cap < (size_t)n3 * sizeof(float2)) {
+    if (e == hipSuccess && p->lo1_n < n3) {  // filled length, set only once the fill is enqueued
       e = p->lo1.ensure((size_t)n3 * sizeof(float2));
       if (e == hipSuccess) e = launch_fill_c64(p->lo1.as<float2>(), n3, 1.f, 0.f, st);
+      if (e == hipSuccess) p->lo1_n = n3;
     }
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   }
@@ -1040,11 +1045,14 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if ((p->path == 4 || p->path == 5) && !pc8 && !head && !pc4 && !pc2)
     return fail(ZFFT_EUNSUPPORTED, "PC decimator needs frames of >= 16384 samples and <= 65535 "
                                    "frames per call");
+  // the tiles hand a batch over to XA only where XA takes it (auto_xa: from 768 frames of
+  // > 2^19 samples), never to the blocked passes, which lose to the tiles at every batch
+  const bool xa_auto = auto_xa(frames, L) && xa_fits(p, L);
   // zoom 2: the tiles on request (paths 4, 5) and automatic below 512 frames per call
-  if (pc2 && (p->path == 4 || p->path == 5 || (p->path == 0 && frames < kPc2TilesMaxFrames)))
+  if (pc2 && (p->path == 4 || p->path == 5 || (p->path == 0 && (frames < kPc2TilesMaxFrames || !xa_auto))))
     return run_pc(p, in, L, frames, n, false, out, st, 1);
   // zoom 4: the walk on request, the tiles on request and automatic below 1024 frames per call
-  if (pc4 && (p->path == 4 || p->path == 5 || (p->path == 0 && frames < kPc4TilesMaxFrames)))
+  if (pc4 && (p->path == 4 || p->path == 5 || (p->path == 0 && (frames < kPc4TilesMaxFrames || !xa_auto))))
     return run_pc(p, in, L, frames, n, p->path == 5, out, st, p->K);
   const bool walk = p->path == 5 || (p->path == 0 && frames >= kPcWalkMinFrames);
   // PC is the fastest schedule wherever it applies, from one frame per call (the
@@ -1340,8 +1348,9 @@ int zfft_plan_destroy(zfft_plan *p) {
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
                     &p->tws, &p->means, &p->z4, &p->winf, &p->pc_tab, &p->pc_edge, &p->pc_tab4,
                     &p->wparts, &p->lo1, &p->pc_tab2, &p->lut_d, &p->rgba, &p->al_hist, &p->al_bins,
-                    &p->edge_v})
+                    &p->edge_v, &p->img64})
     b->release();
+  if (p->row_pin) (void)hipHostFree(p->row_pin);
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
   if (p->done_ev) (void)hipEventDestroy(p->done_ev);
   if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
@@ -1478,7 +1487,9 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
   // batch k+1 while the GPU computes batch k.  Every batch takes the schedule its own frame
   // count earns; a call the XA tiles would take keeps them in every batch: its batches hold at
   // least the XA threshold for this frame length (or the call is one batch), so splitting
-  // never drops a large call onto a schedule that loses at its batch size.
+  // never drops a large call onto a schedule that loses at its batch size.  At zoom 4 and 2 a
+  // batch below the tiles' crossover (1024 / 512 frames) takes the tiles, which is what its
+  // own frame count earns (e.g. 3000 cfg1 frames: batches of 1000 run the zoom-4 tiles).
   int B = frames;
   const size_t total = (size_t)frames * frame_bytes;
   if (total >= kPipeMinBytes && frames >= 2) {
@@ -1674,34 +1685,118 @@ int zfft_waterfall_get_levels(const zfft_plan *p, double *minlev, double *maxlev
   return ZFFT_OK;
 }
 
+namespace {
+// The colormap LUT on the device (built and uploaded on first use, on st) and makeARGB's
+// levels (pyqtgraph functions.py): equal levels -> max = nextafter(max, 2 max); scale = lut
+// size / (max - min) (1 when the range is 0)
+int render_setup(zfft_plan *p, hipStream_t st, double *lo, double *scale) {
+  if (!p->lut_ready) {
+    build_lut(p->cmap.c_str(), p->lut);
+    p->lut_ready = true;
+  }
+  if (!p->lut_uploaded) {
+    hipError_t e = p->lut_d.ensure(sizeof(p->lut));
+    if (e == hipSuccess) e = hipMemcpyAsync(p->lut_d.p, p->lut, sizeof(p->lut), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(e, "LUT upload");
+    p->lut_uploaded = true;
+  }
+  double l = p->lev_lo, h = p->lev_hi;
+  if (l == h) h = std::nextafter(h, 2.0 * h);
+  double rng = h - l;
+  if (rng == 0.0) rng = 1.0;
+  *lo = l;
+  *scale = 256.0 / rng;
+  return ZFFT_OK;
+}
+
+// zfft_waterfall_push_render / _push_read64: count host rows pushed, then the image emitted
+// (RGBA8 or float64) and copied to the host -- one kernel for the per-line case, one copy, one
+// wait.  The rows are staged in page-locked memory the kernels read in place.
+constexpr size_t kDisplayZeroCopyMax = (size_t)4 << 20;
+int push_emit(zfft_plan *p, const float *rows, int32_t count, bool f64, void *host_out) {
+  int rc = enter(p);
+  if (rc) return rc;
+  if (!host_out) return fail(ZFFT_EINVAL, "null output");
+  if (count < 0 || (count > 0 && !rows)) return fail(ZFFT_EINVAL, "bad rows / count");
+  rc = ensure_waterfall(p);
+  if (rc) return rc;
+  const int H = p->H, W = p->W;
+  const size_t npx = (size_t)H * W, bytes = npx * (f64 ? sizeof(double) : 4);
+  hipError_t e = f64 ? p->img64.ensure(bytes) : p->rgba.ensure(bytes);
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "image buffer allocation failed");
+  const float *drows = nullptr;
+  if (count > 0) {
+    const size_t rb = (size_t)count * W * sizeof(float);
+    if (rb > p->row_pin_cap) {
+      if (p->row_pin) (void)hipHostFree(p->row_pin);
+      p->row_pin = nullptr;
+      p->row_pin_cap = 0;
+      e = hipHostMalloc((void **)&p->row_pin, rb, hipHostMallocDefault);
+      if (e != hipSuccess) return fail(ZFFT_ENOMEM, "page-locked row staging allocation failed");
+      p->row_pin_cap = rb;
+    }
+    // every display call waits for its kernels before returning: no kernel still reads row_pin
+    std::memcpy(p->row_pin, rows, rb);
+    void *d = nullptr;
+    e = hipHostGetDevicePointer(&d, p->row_pin, 0);
+    if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+    drows = (const float *)d;
+  }
+  rc = use_stream(p, p->stream);
+  if (rc) return rc;
+  double lo = 0.0, scale = 1.0;
+  if (!f64) {
+    rc = render_setup(p, p->stream, &lo, &scale);
+    if (rc) return rc;
+  }
+  // a small image into page-locked host memory is written by the kernel in place (no copy
+  // command: the UI's widths, W <= 1024, are 64 KB .. 1 MB per image); a large one goes through
+  // the device buffer and one DMA copy (at W = 8192 the 67 MB RGBA image copies faster so)
+  void *dout = f64 ? p->img64.p : p->rgba.p;
+  void *hout = nullptr;
+  if (bytes <= kDisplayZeroCopyMax && hipHostGetDevicePointer(&hout, host_out, 0) == hipSuccess && hout)
+    dout = hout;
+  else
+    (void)hipGetLastError(), hout = nullptr;
+  if (count > 1) {  // the batch through the push kernels, then the image
+    e = launch_waterfall_push(p->ring.as<float>(), H, W, drows, W, count, p->off, p->cfg.scroll, p->stream);
+    if (e != hipSuccess) return hip_fail(e, "waterfall push");
+    p->off = ((p->off + (int64_t)count * p->cfg.scroll) % H + H) % H;
+    drows = nullptr;
+  }
+  e = launch_waterfall_push_emit(p->ring.as<float>(), H, W, p->off, p->cfg.scroll, drows, p->lut_d.p, lo,
+                                 scale, dout, f64, p->stream);
+  if (e != hipSuccess) return hip_fail(e, "waterfall push + emit");
+  if (drows) p->off = ((p->off + p->cfg.scroll) % H + H) % H;
+  if (!hout) e = hipMemcpyAsync(host_out, dout, bytes, hipMemcpyDeviceToHost, p->stream);
+  if (e == hipSuccess) e = done_on(p, p->stream) == ZFFT_OK ? hipSuccess : hipErrorUnknown;
+  if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+  return e == hipSuccess ? ZFFT_OK : hip_fail(e, "waterfall image copy");
+}
+}  // namespace
+
+int zfft_waterfall_push_render(zfft_plan *p, const float *rows, int32_t count, uint8_t *rgba_out) {
+  return push_emit(p, rows, count, false, rgba_out);
+}
+
+int zfft_waterfall_push_read64(zfft_plan *p, const float *rows, int32_t count, double *img_out) {
+  return push_emit(p, rows, count, true, img_out);
+}
+
 int zfft_waterfall_render_device(zfft_plan *p, uint8_t *d_rgba, void *hip_stream) {
   int rc = enter(p);
   if (rc) return rc;
   if (!d_rgba) return fail(ZFFT_EINVAL, "null output");
   rc = ensure_waterfall(p);
   if (rc) return rc;
-  hipError_t e = hipSuccess;
-  if (!p->lut_ready) {
-    build_lut(p->cmap.c_str(), p->lut);
-    p->lut_ready = true;
-  }
   hipStream_t st = pick_stream(p, hip_stream);
   rc = use_stream(p, st);
   if (rc) return rc;
-  if (!p->lut_uploaded) {
-    e = p->lut_d.ensure(sizeof(p->lut));
-    if (e == hipSuccess) e = hipMemcpyAsync(p->lut_d.p, p->lut, sizeof(p->lut), hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hip_fail(e, "LUT upload");
-    p->lut_uploaded = true;
-  }
-  // makeARGB levels (pyqtgraph functions.py): equal levels -> max = nextafter(max, 2 max);
-  // scale = lut size / (max - min) (1 when the range is 0)
-  double lo = p->lev_lo, hi = p->lev_hi;
-  if (lo == hi) hi = std::nextafter(hi, 2.0 * hi);
-  double rng = hi - lo;
-  if (rng == 0.0) rng = 1.0;
-  e = launch_waterfall_render(p->ring.as<float>(), p->H, p->W, p->off, p->lut_d.p, lo, 256.0 / rng,
-                              d_rgba, st);
+  double lo, scale;
+  rc = render_setup(p, st, &lo, &scale);
+  if (rc) return rc;
+  hipError_t e = launch_waterfall_render(p->ring.as<float>(), p->H, p->W, p->off, p->lut_d.p, lo, scale,
+                                         d_rgba, st);
   if (e != hipSuccess) return hip_fail(e, "waterfall render");
   return done_on(p, st);
 }

@@ -110,6 +110,18 @@ class Waterfall:
     reference's image exactly for float32-representable rows and within half a float32 ulp
     (<= 7.6e-6 dB for |dB| < 256) otherwise; the grid stamps (0) and the -500 fill are exact.
     Pinned by tests/test_gpu_parity.py::test_waterfall_float64_rows_are_held_as_float32.
+
+    `image_update` stages the row on the host; the device push happens with the next read of
+    the image (`img_array`, `render`, `autolevel`), together with that read in one round trip
+    (zfft_waterfall_push_read64 / _push_render: one kernel, one copy, one wait per line), or
+    when H rows are pending.  The image returned is the same as with a push per call.
+
+    Buffer reuse: `img_array` and `render()` return one of two page-locked arrays this
+    Waterfall owns and uses in turn, so an array stays valid until the read after next (what
+    pyqtgraph's setImage per line needs: it copies or draws at once).  A caller that keeps
+    images (recording, diffing, handing them to another thread) copies them, or passes its
+    own array as `out=` to `render` / `image(out=...)`.  Like the reference's class, one
+    Waterfall is for one thread.
     """
 
     def __init__(self, scroll: int = 1, device: int = 0, fs: float = 2.4e6):
@@ -120,9 +132,11 @@ class Waterfall:
         self._plan: ZoomFFT | None = None
         self._cmap = "Default"
         self._levels = (-220.0, -120.0)  # Waterfall.__init__ (S:1593-1598)
+        self._pending: list[np.ndarray] = []  # rows image_update staged for the next read
 
     def _ensure(self, width: int):
         if width != self.fftwidth or self._plan is None:
+            self._pending = []  # a new width re-inits the image (S:1632-1636)
             if self._plan is not None:
                 self._plan.close()
             n_fft = 1 << max(5, (width - 1).bit_length())
@@ -133,11 +147,25 @@ class Waterfall:
             self.fftwidth = width
 
     def init_image(self):
+        self._pending = []
         if self._plan is not None:
             self._plan.waterfall_reset(self.scroll)
 
+    def _take_pending(self):
+        n = len(self._pending)
+        rows = None if n == 0 else self._pending[0] if n == 1 else np.stack(self._pending)
+        self._pending = []
+        return rows
+
+    def flush(self) -> None:
+        """Push the staged rows to the device ring now (no image read)."""
+        if self._plan is not None:
+            for r in self._take_pending() if self._pending else ():
+                self._plan.waterfall_push(r)
+
     def close(self):
         """Release the device ring (the reference's image is garbage-collected)."""
+        self._pending = []
         if self._plan is not None:
             self._plan.close()
             self._plan = None
@@ -153,13 +181,19 @@ class Waterfall:
         self._ensure(width)
         for x in (0, width // 2, width - 1):
             psd[x] = 0
-        self._plan.waterfall_push(np.asarray(psd, dtype=np.float32))
+        self._pending.append(np.array(psd, dtype=np.float32).reshape(width))
+        if len(self._pending) >= max(1, width // 4):  # H rows: the oldest would scroll out
+            self.flush()
+
+    def image(self, out: np.ndarray | None = None) -> np.ndarray:
+        """The float64 (H, W) image in the reference's row order, staged rows pushed first."""
+        if self._plan is None:
+            raise AttributeError("img_array is created by the first image_update")
+        return self._plan.waterfall_push_emit(self._take_pending(), True, out)
 
     @property
     def img_array(self) -> np.ndarray:
-        if self._plan is None:
-            raise AttributeError("img_array is created by the first image_update")
-        return self._plan.waterfall_image().astype(np.float64)
+        return self.image()
 
     # ---- rendering (SURVEY §8f-2): Waterfall.lookuptable / newlevel / autolevel, and the
     #      RGBA image pyqtgraph's ImageItem draws from img_array (S:1579-1623, 1667-1685)
@@ -184,16 +218,19 @@ class Waterfall:
     def autolevel(self):
         """Levels from the 2nd / 98th percentiles of the pixels below 0 (what S:1676
         computes; the reference stores them in unused attributes, so its button is a no-op)."""
-        self._levels = self._need_plan().waterfall_autolevel()
+        plan = self._need_plan()
+        self.flush()
+        self._levels = plan.waterfall_autolevel()
         return self._levels
 
     @property
     def levels(self):
         return self._plan.waterfall_levels() if self._plan is not None else self._levels
 
-    def render(self) -> np.ndarray:
-        """RGBA uint8 (H, W, 4) in img_array's row order."""
-        return self._need_plan().waterfall_render()
+    def render(self, out: np.ndarray | None = None) -> np.ndarray:
+        """RGBA uint8 (H, W, 4) in img_array's row order, staged rows pushed first (one
+        round trip); see the class docstring for the reuse of the returned array."""
+        return self._need_plan().waterfall_push_emit(self._take_pending(), False, out)
 
 
 class Data:

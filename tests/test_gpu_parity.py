@@ -193,6 +193,65 @@ def test_waterfall_batch_push_matches_sequence(W, scroll):
                                           err_msg=f"W={W} scroll={scroll} K={K}")
 
 
+@pytest.mark.parametrize("W", [64, 512])
+@pytest.mark.parametrize("scroll", [1, -1])
+def test_waterfall_push_emit_matches_separate_calls(W, scroll):
+    """zfft_waterfall_push_render / _push_read64 (rows pushed and the image read in one
+    round trip; one fused kernel for a single row) give bit for bit what zfft_waterfall_push
+    then zfft_waterfall_render / zfft_waterfall_read give, for 0, 1, 3, H and H + 2 rows per
+    call, across a scroll inversion, with NaN pixels and non-default levels."""
+    from pypanadapter_amd import ZoomFFT
+    H = W // 4
+    rng = np.random.default_rng(3 * W + scroll)
+    kw = dict(n_win=W, scroll=scroll)
+    with ZoomFFT(4096, 1, 2.4e6, **kw) as a, ZoomFFT(4096, 1, 2.4e6, **kw) as b:
+        for p in (a, b):
+            p.waterfall_colormap("Tropical")
+            p.waterfall_levels(-190.0, -115.0)
+        sc = scroll
+        for step, K in enumerate([1, 1, 0, 3, 1, H, 1, H + 2, 1, 1]):
+            if step == 6:  # the reference's scroll inversion (S:2074-2077) mid-sequence
+                sc = -sc
+                a.waterfall_reset(sc)
+                b.waterfall_reset(sc)
+            rows = rng.uniform(-200, -100, (K, W)).astype(np.float32)
+            if K:
+                rows[0, 5] = np.nan
+            for r in rows:
+                b.waterfall_push(r)
+            f64 = step % 2 == 1
+            got = a.waterfall_push_emit(rows if K else None, f64, out=None).copy()
+            want = b.waterfall_image().astype(np.float64) if f64 else b.waterfall_render().copy()
+            np.testing.assert_array_equal(got, want, err_msg=f"W={W} scroll={scroll} step={step} K={K}")
+        np.testing.assert_array_equal(a.waterfall_image(), b.waterfall_image())
+
+
+def test_waterfall_facade_deferred_reads_follow_the_reference():
+    """The facade stages image_update rows and pushes them with the next image read: reading
+    img_array / render after every line, after every few lines and across a width change (a
+    new image) follows the reference's image_update sequence exactly; autolevel sees the
+    staged rows."""
+    from oracle import render as rr
+    from oracle.scipy_path import Waterfall as RefWaterfall
+    from pypanadapter_amd import Waterfall
+    rng = np.random.default_rng(77)
+    w, ref = Waterfall(scroll=1), RefWaterfall()
+    for k in range(60):
+        W = 128 if k < 45 else 256
+        row = rng.uniform(-200.0, -110.0, W).astype(np.float32).astype(np.float64)
+        w.image_update(row.copy())
+        ref.image_update(row.copy(), 1)
+        if k % 7 == 0 or k > 50:
+            np.testing.assert_array_equal(w.img_array, ref.img_array, err_msg=f"line {k}")
+        if k % 11 == 3:
+            np.testing.assert_array_equal(w.render(), rr.render(ref.img_array, rr.lookup_table("Default"),
+                                                                w.levels), err_msg=f"render {k}")
+    w.image_update(rng.uniform(-200.0, -110.0, 256))
+    lv = w.autolevel()
+    assert lv == rr.autolevel(w.img_array)
+    w.close()
+
+
 def _frames(F, L, N, z, W, seed0=100, fs=2.4e6, f_lo=1.0):
     from pypanadapter_amd import synth
     return np.stack([synth.make_iq(L, fs, seed0 + f, n_fft=N, zoom=z, n_win=W, f_lo=f_lo)
@@ -429,6 +488,7 @@ def test_facade_matches_reference_rows():
                                         (4, 384, 262144, "pc"), (4, 64, 1048576, "pc"),
                                         (4, 1023, 65536, "pc"), (4, 1024, 65536, "xa"),
                                         (2, 512, 65536, "xa"), (2, 511, 65536, "pc2"), (2, 8, 262144, "pc2"),
+                                        (2, 600, 1048576, "pc2"), (2, 768, 1048576, "xa"),
                                         (2, 8, 8192, "exact"),
                                         (16, 384, 262144, "pc"), (16, 512, 262144, "pc"),
                                         (16, 8, 262144, "pc")])
@@ -440,7 +500,8 @@ def test_auto_schedule_by_batch(z, F, L, want):
     from 4096 frames per call; zoom >= 16 as PC's first three stages + XA where XA would take
     the batch and zoom 2's tiles does not (>= 512 frames; zoom 2's tiles below that, then the
     blocked passes under 16384 samples); PC's tiles at zoom 4
-    below 1024 frames per call and at zoom 2 below 512, XA from there; for frames < 16384 samples
+    below 1024 frames per call and at zoom 2 below 512, XA from there where XA takes the batch (the
+    tiles, not the blocked passes, for 512-767 frames of > 2^19 samples); for frames < 16384 samples
     >= 384 frames of <= 2^19 samples (768 of longer ones) the XA tiles and smaller batches the
     exact blocked passes (the fused interior with edge windows is reached on request only)."""
     import torch

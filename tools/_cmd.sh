@@ -1,5 +1,8 @@
-# Scratch GPU command of the current session (run as: gpurun -- 'bash tools/_cmd.sh'):
-# cfg5 PMC traffic (complex64, complex32) at the final sources, and the schedule sweep.
+# Scratch GPU command of the current session (run as: gpurun -- 'bash tools/_cmd.sh').
 set -u
 export TMPDIR=/tmp
-bash tools/gpu_session.sh r05fin6b pmc5
+TESTK="tests/test_render.py tests/test_gpu_parity.py" bash tools/gpu_session.sh r06g tests_k || exit $?
+mkdir -p gpurun_out/r06g
+timeout -k 10 300 python -c "
+import json, torch, bench
+print(json.dumps(bench.display_timing(torch.device('cuda:0')), indent=1))" > gpurun_out/r06g/display.log 2>&1; cat gpurun_out/r06g/display.log
