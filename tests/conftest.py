@@ -59,6 +59,28 @@ def row_errors(row, ref):
     return ddb, damp
 
 
+# Tolerance ledger: the largest relative error each decimated-IQ check measured, by key, so the
+# bounds can be set from measurements.  Written at the end of the session
+# to $ZFFT_TOL_LEDGER when that is set (tools/gpu_session.sh "ledger").
+_LEDGER = {}
+
+
+def check_rel(got, ref, bound, key, what=""):
+    """max |got - ref| / max |ref| < bound, recorded under `key`."""
+    err = np.abs(np.asarray(got) - ref) / np.abs(ref).max()
+    e = float(err.max())
+    _LEDGER[key] = max(_LEDGER.get(key, 0.0), e)
+    assert e < bound, (key, what, e, int(err.argmax()), len(err))
+    return e
+
+
+def pytest_sessionfinish(session, exitstatus):
+    path = os.environ.get("ZFFT_TOL_LEDGER")
+    if path and _LEDGER:
+        with open(path, "w") as fh:
+            json.dump({k: _LEDGER[k] for k in sorted(_LEDGER)}, fh, indent=1)
+
+
 def assert_row_close(row, ref, what="", db_tol=DB_TOL, amp_tol=AMP_TOL):
     ddb, damp = row_errors(row, ref)
     assert ddb <= db_tol and damp <= amp_tol, f"{what}: max|ddB|={ddb:.3e} max|damp|={damp:.3e}"

@@ -2,16 +2,24 @@
 the float64 oracle of the reference's decimate(x, 2) x 3 (pypanadapter_spectrum.py:2096-2098)
 and its rows, and against the golden rows recorded from the reference.
 
-Decimated IQ: relative to the output peak, PC's fp32 error is ~2-3e-6 (tools/pc_model.py:
-FIRs + own-rate sections + output-rate sections + frame-end maps); the bound here is XA's
-documented 1e-5 per stage... taken once (1e-5) for the whole cascade.  Rows: the §8(c) gate."""
+Decimated IQ: relative to the output peak, PC's fp32 error is 2-6e-6 (the bounds below are
+the measured worst + ~20 %, from the tolerance ledger).  Rows: the §8(c) gate."""
 import numpy as np
 import pytest
 
-from conftest import assert_row_close, case_input, golden_cases, golden_rows
+from conftest import assert_row_close, case_input, check_rel, golden_cases, golden_rows
 
 pytestmark = pytest.mark.gpu
-PC_TOL = 1e-5
+# Bounds = the largest error measured over every check below on the shipped kernels (the
+# tolerance ledger, profiles/r06h/tol_ledger.json; tests/conftest.py check_rel) + ~20 %:
+#   PC_TOL    zoom 8 / 4 / 2 decimated IQ vs the float64 oracle, and PC vs XA: worst 5.35e-6
+#             (zoom 8, tiles); the walk on the zf_n512_z8 fixture 6.07e-6 (test_gpu_parity)
+#   HEAD_TOL  zoom >= 16 (PC's x8, then zoom 2's tiles or the blocked passes): worst 6.02e-6
+#   CMP_TOL   PC against the exact blocked passes (two fp32 paths, errors add): worst 7.10e-6
+# DESIGN §3.5 has where PC's 5-6e-6 comes from (the FIR taps summed in order).
+PC_TOL = 6.5e-6
+HEAD_TOL = 7.5e-6
+CMP_TOL = 8.6e-6
 # 4: K1 + K2 tiles (y2 through device memory), 5: KW (one workgroup walks each frame)
 PC_PATHS = pytest.mark.parametrize("path", [4, 5], ids=["tiles", "walk"])
 
@@ -47,8 +55,7 @@ def test_pc_decimate_vs_oracle(oracle_lib, flip, path):
             d = plan.decimate(x)
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 8, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
-        err = np.abs(d - ref) / np.abs(ref).max()
-        assert err.max() < PC_TOL, (L, flip, float(err.max()), int(err.argmax()), len(d))
+        check_rel(d, ref, PC_TOL, f"pc8/decimate/path{path}", (L, flip))
 
 
 @pytest.mark.parametrize("N,L,F", [(4096, 299008, 6), (16384, 294912, 3), (65536, 1048576, 2),
@@ -144,8 +151,7 @@ def test_pc_matches_xa_and_exact_rows(oracle_lib):
             plan.set_path(path)
             out[path] = (plan.rows(x), plan.decimate(x[1]))
     for p in (4, 5):
-        a, b = out[p][1], out[1][1]
-        assert np.abs(a - b).max() / np.abs(b).max() < PC_TOL
+        check_rel(out[p][1], out[1][1], CMP_TOL, f"pc8/vs_exact_path/path{p}")
     for f in range(4):
         ref = oracle_lib.psd_row(x[f], 2.4e6, 4096, 8, 512)
         for path in (1, 3, 4, 5):
@@ -245,8 +251,7 @@ def test_pc_head_decimate_vs_oracle(oracle_lib, zoom, flip, path):
         assert names.count("pc_tail") == tiles + (path == 4), (L, names)
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, zoom, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
-        err = np.abs(d - ref) / np.abs(ref).max()
-        assert err.max() < 2 * PC_TOL, (L, zoom, flip, float(err.max()), int(err.argmax()), len(d))
+        check_rel(d, ref, HEAD_TOL, f"head/zoom{zoom}/path{path}", (L, flip))
 
 
 @PC_PATHS
@@ -308,8 +313,7 @@ def test_pc2_decimate_vs_oracle(oracle_lib, flip):
         assert names[-1] == "pc_edge", names  # (decimate marks no start: its first launch is unnamed)
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 2, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
-        err = np.abs(d - ref) / np.abs(ref).max()
-        assert err.max() < PC_TOL, (L, flip, float(err.max()), int(err.argmax()), len(d))
+        check_rel(d, ref, PC_TOL, "pc2/decimate", (L, flip))
 
 
 @pytest.mark.parametrize("N,L,F", [(2048, 262144, 4), (4096, 299008, 3), (1024, 65536 + 1, 5)])
@@ -380,7 +384,7 @@ def test_pc2_size_independent_properties():
     np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(c, a[perm])
     np.testing.assert_allclose(d - a, 20 * np.log10(4.0), atol=2e-4)
-    assert np.abs(da - dx).max() / np.abs(dx).max() < 2 * PC_TOL
+    check_rel(da, dx, PC_TOL, "pc2/vs_xa")
     np.testing.assert_allclose(xa, a, atol=2e-3)
 
 
@@ -404,8 +408,7 @@ def test_pc4_decimate_vs_oracle(oracle_lib, flip, path):
             d = plan.decimate(x)
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 4, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
-        err = np.abs(d - ref) / np.abs(ref).max()
-        assert err.max() < PC_TOL, (L, flip, float(err.max()), int(err.argmax()), len(d))
+        check_rel(d, ref, PC_TOL, f"pc4/decimate/path{path}", (L, flip))
 
 
 @pytest.mark.parametrize("N,L,F", [(1024, 262144, 5), (4096, 299008, 3), (2048, 131072 + 3, 4)])
@@ -478,5 +481,5 @@ def test_pc4_size_independent_properties(path):
     np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(c, a[perm])
     np.testing.assert_allclose(d - a, 20 * np.log10(4.0), atol=2e-4)
-    assert np.abs(da - dx).max() / np.abs(dx).max() < 2 * PC_TOL
+    check_rel(da, dx, PC_TOL, "pc4/vs_xa")
     np.testing.assert_allclose(xa, a, atol=2e-3)
