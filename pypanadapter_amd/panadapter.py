@@ -159,8 +159,8 @@ class Waterfall:
 
     def flush(self) -> None:
         """Push the staged rows to the device ring now (no image read)."""
-        if self._plan is not None:
-            for r in self._take_pending() if self._pending else ():
+        if self._plan is not None and self._pending:
+            for r in np.atleast_2d(self._take_pending()):
                 self._plan.waterfall_push(r)
 
     def close(self):

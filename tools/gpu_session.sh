@@ -36,6 +36,11 @@ for s in $STEPS; do
       run pytest_k 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --timeout 300 --timeout-method thread ${TESTK}
       rc=$?
       [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
+    ledger)  # every GPU test, with the tolerance ledger (largest error per check) written
+      ZFFT_TOL_LEDGER="$OUT/tol_ledger.json" run pytest_ledger 1100 python -u -m pytest tests -m gpu -q \
+        -p no:cacheprovider -rf --timeout 300 --timeout-method thread
+      rc=$?
+      [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     smoke)
       run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
