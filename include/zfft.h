@@ -211,8 +211,9 @@ int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *coun
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
 /* Decimator schedule: 0 = automatic -- for zoom 8 and frames of >= 16384 samples 4 below
- * 4096 frames per call and 5 from there (zoom >= 16: the same for the first three stages;
- * zoom 4: 4 below 1024 frames per call, zoom 2 below 512); otherwise 3 for batches of >= 768 frames, or >= 384 frames of <= 2^19
+ * 1024 frames per call and 5 from there (zoom >= 16: the same for the first three stages;
+ * zoom 4: 4 below 512 frames per call and 5 from there; zoom 2: 4 below 512); otherwise 3 for
+ * batches of >= 768 frames, or >= 384 frames of <= 2^19
  * samples, else 2 for batches of >= 2^27 samples whose frames are long enough for the edge
  * windows, else 1 -- e.g. one frame per call, the reference's use.  Each batch of a
  * zfft_process call is judged by its own frame count (host calls are split into batches of
@@ -233,10 +234,10 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * rank-~10 frame-end maps; frames >= 16384 samples, <= 65535 frames per launch; zoom 4, 2
  * and the head of zoom >= 16 as below), 5 = the
  * same arithmetic as one launch with one workgroup per frame (the rate-1/4 intermediate
- * stays on chip; automatic from 4096 frames per call); at zoom 4, path 5 is the two-stage
+ * stays on chip; automatic from 1024 frames per call); at zoom 4, path 5 is the two-stage
  * form of the walk (FIR, own-rate sections at rate 1/2, 41-tap FIR, 6 output-rate sections;
- * on request only: XA is faster there) and path 4 its tiles (automatic below 1024 frames per
- * call, XA from there); at zoom 2, paths 4 / 5 run one-stage tiles in XA's factorisation (the
+ * automatic from 512 frames per call) and path 4 its tiles (automatic below that); at zoom 2,
+ * paths 4 / 5 run one-stage tiles in XA's factorisation (the
  * 4 sections forward at the input rate, a 25-tap FIR, their squares backward at half rate;
  * automatic below 512 frames per call); at zoom >= 16, paths 4 / 5 run PC (tiles / walk) for the
  * first three stages and XA for the rest on its 1/8-rate output -- the automatic choice

@@ -793,28 +793,32 @@ int run_xa(zfft_plan *p, const InDesc &in, int frames, const std::vector<int64_t
 // maps do not meet (kPcMinL), grid y = frames.
 constexpr int64_t kPcMinL = 16384;
 // KW (one workgroup per frame) from this many frames per call; below, K1 + K2's tiles.
-// tools/sweep_schedule.py (KW / tiles time per call, 299,008-sample frames): 64 frames 3.2,
-// 512 1.00, 2048 0.99, 4096 1.01 (profiles/r04r; r04l: 0.987), and 0.96 on bench.py's
-// steady-state clock at 4096 (profiles/r04p): one workgroup per frame needs several rounds of
-// the chip's 512 resident workgroups to fill it; KW also keeps y2 (2 B per input sample,
-// 6 GB per cfg2 step with its read-back) off HBM.
-constexpr int kPcWalkMinFrames = 4096;
+// tools/sweep_walk.py (profiles/r06k/sweep_walk.json, round 6's walk; ms per call, tiles / walk):
+// 299,008-sample frames 512: 0.78 / 0.78, 768: 1.08 / 1.12, 1024: 1.44 / 1.43, 2048: 2.64 /
+// 2.53, 4096: 5.21 / 4.87; 2^20-sample frames 768: 3.34 / 3.44, 1024: 4.40 / 4.36, 2048: 8.54 /
+// 8.27 (cfg5), 4096: 16.8 / 16.0.  One workgroup per frame needs about two rounds of the chip's
+// 512 resident workgroups to fill it; KW also keeps y2 (2 B per input sample) off HBM.  (Round
+// 4 measured the walk level with the tiles up to 4096 frames: the threshold was 4096.)
+constexpr int kPcWalkMinFrames = 1024;
+// Zoom 4: the two-stage walk from this many frames per call, the tiles below; XA no longer
+// wins anywhere PC fits (cfg1's 262,144-sample frames, ms per call, XA / tiles / walk: 256:
+// 1.24 / 0.47 / 0.50, 512: 1.32 / 0.90 / 0.78, 1024: 1.69 / 1.69 / 1.44, 4096 (cfg1): 5.17 /
+// 6.27 / 4.89; profiles/r06k/sweep_walk.json).
+constexpr int kPc4WalkMinFrames = 512;
 bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == kPcStages && L >= kPcMinL && frames <= 65535;
 }
-// Zoom 4 (two stages): the walk (pc_walk_kernel<4>, path 5, on request: at cfg1 -- F = 4096,
-// L = 262,144 -- it takes 4.49-4.50 ms against XA's 2.89 + 1.45 = 4.34 ms on the same box,
-// profiles/r05h: at zoom 4 the recurrences run on twice the share of the samples they see at
-// zoom 8, and they are the walk's latency-bound half) and the tiles (K1 = FIR alpha into y1,
-// K2 = the zoom-8 tail kernel on zoom 4's tables: path 4, and automatic below XA's batch).
+// Zoom 4 (two stages): the walk (pc_walk_kernel<4>, path 5, automatic from kPc4WalkMinFrames:
+// round 5's form lost to XA at cfg1, 4.49 against 4.34 ms, profiles/r05h; round 6's walk wins)
+// and the tiles (K1 = FIR alpha into y1, K2 = the zoom-8 tail kernel on zoom 4's tables: path 4,
+// automatic below the walk's batch).
 bool pc4_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == 2 && L >= kPcMinL && frames <= 65535;
 }
 // Zoom-4 tiles against XA (cfg1's 262,144-sample frames, profiles/r05u, ms per call): 1 frame
 // 0.061 / 1.14 (blocked passes 0.22), 64: 0.14 / 1.21 (0.28), 256: 0.46 / 1.24, 384: 0.65 /
-// 1.26, 1024: 1.64 / 1.56 -- XA, one wave per frame, needs about a thousand frames to fill the
-// chip.
-constexpr int kPc4TilesMaxFrames = 1024;
+// 1.26 -- XA, one wave per frame, needs about a thousand frames to fill the chip; from 512
+// frames the zoom-4 walk beats both (kPc4WalkMinFrames).
 // Zoom 2 (one stage): the tail kernel on the mixed input in XA's factorisation (D forward at
 // the input rate, the 25-tap FIR M, D2 backward at half rate), automatic below
 // 512 frames per call: cfg2's 299,008-sample frames, ms per call, tiles / XA (profiles/r05y):
@@ -1051,9 +1055,10 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   // zoom 2: the tiles on request (paths 4, 5) and automatic below 512 frames per call
   if (pc2 && (p->path == 4 || p->path == 5 || (p->path == 0 && (frames < kPc2TilesMaxFrames || !xa_auto))))
     return run_pc(p, in, L, frames, n, false, out, st, 1);
-  // zoom 4: the walk on request, the tiles on request and automatic below 1024 frames per call
-  if (pc4 && (p->path == 4 || p->path == 5 || (p->path == 0 && (frames < kPc4TilesMaxFrames || !xa_auto))))
-    return run_pc(p, in, L, frames, n, p->path == 5, out, st, p->K);
+  // zoom 4: the tiles below 512 frames per call, the walk from there (both on request too)
+  if (pc4 && (p->path == 4 || p->path == 5 || p->path == 0))
+    return run_pc(p, in, L, frames, n, p->path == 5 || (p->path == 0 && frames >= kPc4WalkMinFrames), out,
+                  st, p->K);
   const bool walk = p->path == 5 || (p->path == 0 && frames >= kPcWalkMinFrames);
   // PC is the fastest schedule wherever it applies, from one frame per call (the
   // reference's use: 0.083 against 0.37 ms for path 1) to full batches (1024 frames: 1.44
@@ -1487,17 +1492,16 @@ int zfft_process(zfft_plan *p, const void *iq, int64_t L, int32_t frames, float 
   // batch k+1 while the GPU computes batch k.  Every batch takes the schedule its own frame
   // count earns; a call the XA tiles would take keeps them in every batch: its batches hold at
   // least the XA threshold for this frame length (or the call is one batch), so splitting
-  // never drops a large call onto a schedule that loses at its batch size.  At zoom 4 and 2 a
-  // batch below the tiles' crossover (1024 / 512 frames) takes the tiles, which is what its
-  // own frame count earns (e.g. 3000 cfg1 frames: batches of 1000 run the zoom-4 tiles).
+  // never drops a large call onto a schedule that loses at its batch size.  At zoom 8 and 4
+  // (PC at every batch) and zoom 2 below 512 frames a batch takes what its own frame count
+  // earns: the tiles below the walk's batch (e.g. 418-frame cfg2 batches run zoom 8's tiles).
   int B = frames;
   const size_t total = (size_t)frames * frame_bytes;
   if (total >= kPipeMinBytes && frames >= 2) {
     int nb = std::max<int64_t>(2, (int64_t)((total + kPipeBatchBytes - 1) / kPipeBatchBytes));
     B = (frames + nb - 1) / nb;
     const int need = L <= kXaShortFrame ? kXaMinFramesShort : kXaMinFrames;
-    if (p->path == 0 && p->K > 0 && !pc_fits(p, L, frames) &&
-        !(pc4_fits(p, L, frames) && frames < kPc4TilesMaxFrames) &&
+    if (p->path == 0 && p->K > 0 && !pc_fits(p, L, frames) && !pc4_fits(p, L, frames) &&
         !(pc2_fits(p, L, frames) && frames < kPc2TilesMaxFrames) && auto_xa(frames, L) && B < need) {
       nb = std::max(1, frames / need);
       B = (frames + nb - 1) / nb;

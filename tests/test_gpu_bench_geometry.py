@@ -1,6 +1,6 @@
 """Parity at the benchmarked geometry itself ("what's weak" 1): the exact batch
 sizes bench.py times -- cfg2 and cfg3 at F = 4096 frames, cfg5 at F = 2048 (9.8 / 9.7 / 17 GB
-of IQ built on the device by bench.make_frames) -- through the auto schedule (XA tiles), with
+of IQ built on the device by bench.make_frames) -- through the auto schedule (round 6: the PC walk for every one of them), with
 sampled frames including the first, both sides of a 64-frame boundary, the middle and the
 last two compared against the float64 oracle under the fp32 gate.  Reaches the
 > 4 GiB input offsets and the grid's last workgroup."""
@@ -44,7 +44,9 @@ def test_bench_batch_rows_vs_oracle(oracle_lib, torch_dev, config, in_dtype):
         names = plan.launch_names()
     assert names[0] in ("xa_stage_mix", "pc_fir", "pc_walk", "pc_walk4"), names  # the schedule the bench times
     if config == "cfg1":
-        assert names[0] == "xa_stage_mix", names  # zoom 4 at F = 4096: XA (the zoom-4 walk is slower)
+        assert names[0] == "pc_walk4", names  # zoom 4 at F = 4096: the walk (round 6, r06k)
+    if config == "cfg5":
+        assert names[0] == "pc_walk", names  # F = 2048 frames of 2^20 samples: the walk (r06k)
     host = rows.cpu().numpy()
     assert np.isfinite(host).all()
     for f in PICK(F):

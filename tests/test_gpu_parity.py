@@ -484,11 +484,12 @@ def test_facade_matches_reference_rows():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("z,F,L,want", [(8, 1, 299008, "pc"), (8, 384, 299008, "pc"),
-                                        (8, 768, 1048576, "pc"), (8, 4096, 32768, "walk"),
-                                        (8, 4095, 32768, "pc"), (8, 4, 8192, "exact"),
+                                        (8, 768, 1048576, "pc"), (8, 1024, 32768, "walk"),
+                                        (8, 1023, 32768, "pc"), (8, 4, 8192, "exact"),
                                         (4, 1, 262144, "pc"), (4, 256, 262144, "pc"),
                                         (4, 384, 262144, "pc"), (4, 64, 1048576, "pc"),
-                                        (4, 1023, 65536, "pc"), (4, 1024, 65536, "xa"),
+                                        (4, 511, 65536, "pc"), (4, 512, 65536, "walk4"),
+                                        (4, 1024, 65536, "walk4"), (4, 768, 8192, "xa"),
                                         (2, 512, 65536, "xa"), (2, 511, 65536, "pc2"), (2, 8, 262144, "pc2"),
                                         (2, 600, 1048576, "pc2"), (2, 768, 1048576, "xa"),
                                         (2, 8, 8192, "exact"),
@@ -499,10 +500,11 @@ def test_auto_schedule_by_batch(z, F, L, want):
     pc_fits / kPcWalkMinFrames / auto_xa / use_fused, tools/sweep_schedule.py,
     profiles/r04l): at zoom 8 the PC polyphase cascade for every batch of frames >= 16384
     samples (one frame per call -- the reference's use -- included), as its walk kernel
-    from 4096 frames per call; zoom >= 16 as PC's first three stages + XA where XA would take
+    from 1024 frames per call (round 6: profiles/r06k/sweep_walk.json); zoom >= 16 as PC's
+    first three stages + XA where XA would take
     the batch and zoom 2's tiles does not (>= 512 frames; zoom 2's tiles below that, then the
-    blocked passes under 16384 samples); PC's tiles at zoom 4
-    below 1024 frames per call and at zoom 2 below 512, XA from there where XA takes the batch (the
+    blocked passes under 16384 samples); at zoom 4 PC's tiles below 512 frames per call and
+    the zoom-4 walk from there; at zoom 2 the tiles below 512, XA from there where XA takes the batch (the
     tiles, not the blocked passes, for 512-767 frames of > 2^19 samples); for frames < 16384 samples
     >= 384 frames of <= 2^19 samples (768 of longer ones) the XA tiles and smaller batches the
     exact blocked passes (the fused interior with edge windows is reached on request only)."""
@@ -519,7 +521,8 @@ def test_auto_schedule_by_batch(z, F, L, want):
         torch.cuda.synchronize()
         names = plan.launch_names()
     first = {"exact": ("exact_forward_mix",), "fused": ("exact_forward_mix",),
-             "xa": ("xa_stage_mix",), "pc": ("pc_fir",), "pc2": ("pc_tail",), "walk": ("pc_walk",)}[want]
+             "xa": ("xa_stage_mix",), "pc": ("pc_fir",), "pc2": ("pc_tail",), "walk": ("pc_walk",),
+             "walk4": ("pc_walk4",)}[want]
     assert names[0] in first, names
     assert ("edge_windows" in names) == (want == "fused"), names
     if z == 16:  # the PC head's tail stage: zoom 2's tiles below 512 frames, else XA's
@@ -587,14 +590,15 @@ def test_xa_refuses_frames_beyond_32bit_offsets():
                                 torch.cuda.current_stream().cuda_stream)
 
 
-@pytest.mark.parametrize("z,F,L,first,waits", [(8, 1024, 32768, "pc_fir", 1), (4, 2100, 32768, "xa_stage_mix", 1),
+@pytest.mark.parametrize("z,F,L,first,waits", [(8, 1024, 32768, "pc_fir", 1), (4, 2100, 32768, "pc_walk4", 1),
                                                 (2, 2100, 32768, "xa_stage_mix", 1), (2, 500, 32768, "pc_tail", 1),
                                                 (4, 500, 32768, "pc_fir", 1)])
 def test_batched_host_call_times_every_batch_with_one_schedule(z, F, L, first, waits):
     """zfft_process splits a >= 64 MB call into batches (H2D of k+1 under compute of k): the
     timings cover every batch, and a call the XA tiles would take keeps them in every batch
     (batches of >= 384 frames for these lengths, or a single batch) instead of splitting into
-    batches too small for them; PC's tiles (zoom 8, zoom 4 below 1024 frames) take any batch."""
+    batches too small for them; PC (zoom 8 and 4: the tiles below the walk's batch, the walk
+    from it) takes any batch by its own frame count."""
     from pypanadapter_amd import ZoomFFT
     x = np.zeros((F, L), np.complex64)
     x[:, ::3] = 1.0
