@@ -78,10 +78,11 @@ constexpr int kKo = 0;
 #define PC_CENSUS 0
 #endif
 
+
 namespace zfft {
 namespace pc {
 
-[[maybe_unused]] constexpr int kPcStampSegs = 9;
+[[maybe_unused]] constexpr int kPcStampSegs = 10;
 #if PC_STAMPS
 __device__ unsigned long long g_pc_stamps[kPcStampSegs + 1];
 #define PC_STAMP(i)                                                                   \
@@ -804,6 +805,7 @@ pc_walk_kernel(InDesc in, const v2f *lo, v2f *out, int64_t n3, typename WalkZ<ZO
       // vmcnt(0) right behind the barrier, exposing every prefetch's round trip); the next
       // tile's first sub-tile is fetched after the own-rate sections' table loads instead
       if (c + 1 < Z::SUB) prefetch(Z::SUB * tau + c + 1);
+      PC_STAMP(9);  // (stamp segment 9: the mix and x to LDS; segment 0 then the barrier wait)
       if constexpr (!(kKo & 64)) __syncthreads();
       PC_STAMP(0);
       v2f acc[8];

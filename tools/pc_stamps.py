@@ -12,9 +12,9 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pypanadapter_amd import ZoomFFT, _lib  # noqa: E402
 
-SEGS = ["x loads+LO+LDS (4 sub)", "FIR alpha (4 sub)", "y1 to LDS (4 sub)", "FIR beta+z (4 sub)",
+SEGS = ["barrier after x to LDS (4 sub)", "FIR alpha (4 sub)", "y1 to LDS (4 sub)", "FIR beta+z (4 sub)",
         "own-rate causal", "own-rate anticausal", "FIR gamma", "output-rate sections",
-        "out staging+stores"]
+        "out staging+stores", "x wait+LO mix+x to LDS (4 sub)"]
 
 
 def main():
