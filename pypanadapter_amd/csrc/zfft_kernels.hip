@@ -791,7 +791,7 @@ __device__ __forceinline__ int dif_bin(int q) {
   return k;
 }
 
-template <int N, bool PRUNE>
+template <int N, bool PRUNE, bool HALF>
 __global__ __launch_bounds__(Dif<N>::NT, PRUNE ? Dif<N>::WAVES_PRUNE : Dif<N>::WAVES_FULL)
 void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__restrict__ win,
                       const v2f *__restrict__ tw, WelchGeom g, float *__restrict__ rows, int frames) {
@@ -897,18 +897,28 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = r < PF ? pf[r] : DIF_X(s, t, r);
     }
+    // the window values requested before the next segment's prefetch: the wait for them (the
+    // vector-memory counter completes in order) then leaves the prefetch in flight (requested
+    // after it, every segment drained its own prefetch right away)
+    float wv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wv[r] = DIF_W(t, r);
+    __builtin_amdgcn_sched_barrier(0);
     const bool more = s + 1 < s1;
     // (addresses from the loop-invariant thread id: computed once, outside the loop)
-    if (more) {  // in flight during this segment's transform
-      if (2 * g.step == N) {
-        // 50 % overlap (scipy's default noverlap): segment s+1's values [0, 8) are this
-        // segment's raw [8, 16) -- only [8, PF) are loaded
-        const int tt = (int)threadIdx.x % T;
+    // In flight during this segment's transform.  Issued on every segment (the last re-reads
+    // its own values, cached): with the loads under a branch the compiler's wait tracking
+    // merged the paths and drained them at the window's wait, so no segment's prefetch stayed
+    // in flight (round 6, the walk's finding).
+    const int sn = more ? s + 1 : s;
+    if constexpr (HALF) {
+      // 50 % overlap (scipy's default noverlap): segment s+1's values [0, 8) are this
+      // segment's raw [8, 16) -- only [8, PF) are loaded
+      const int tt = (int)threadIdx.x % T;
 #pragma unroll
-        for (int r = 0; r < PF; ++r) pn[r] = r < 8 ? v[r + 8] : DIF_X(s + 1, tt, r);
-      } else {
-        load_seg(pn, s + 1, (int)threadIdx.x % T);
-      }
+      for (int r = 0; r < PF; ++r) pn[r] = r < 8 ? v[r + 8] : DIF_X(sn, tt, r);
+    } else {
+      load_seg(pn, sn, (int)threadIdx.x % T);
     }
     {
       v2f sum = splat(0.f);
@@ -916,7 +926,7 @@ void welch_dif_kernel(const v2f *__restrict__ x, int64_t len, const float *__res
       for (int w = 0; w < D::NW; ++w) sum += red[fl][s & 1][w];
       const v2f mean = sum * (1.f / (float)N);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = (v[r] - mean) * DIF_W(t, r);
+      for (int r = 0; r < 16; ++r) v[r] = (v[r] - mean) * wv[r];
     }
     // stage 1: DFT16 over the thread's own samples, twiddle, store at t + T k
     dft<16>(v);
@@ -1019,20 +1029,27 @@ static hipError_t welch_dif_launch(const float2 *x, int64_t len, const float *wi
   using D = Dif<N>;
   const size_t lds = (size_t)D::FPB * D::SLOTS * sizeof(v2f);
   const bool prune = !g.onesided && g.n_win <= 2 * N / D::RL;
-  const void *k = prune ? (const void *)welch_dif_kernel<N, true> : (const void *)welch_dif_kernel<N, false>;
-  static bool attr_set[2] = {false, false};
-  if (lds > 48 * 1024 && !attr_set[prune]) {
-    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const bool half = 2 * g.step == N;
+  const void *const ks[2][2] = {{(const void *)welch_dif_kernel<N, false, false>, (const void *)welch_dif_kernel<N, false, true>},
+                                {(const void *)welch_dif_kernel<N, true, false>, (const void *)welch_dif_kernel<N, true, true>}};
+  static bool attr_set[2][2] = {};
+  if (lds > 48 * 1024 && !attr_set[prune][half]) {
+    hipError_t e = hipFuncSetAttribute(ks[prune][half], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attr_set[prune] = true;
+    attr_set[prune][half] = true;
   }
   const dim3 grid((unsigned)((frames + D::FPB - 1) / D::FPB), (unsigned)g.split), block(D::NT);
-  if (prune)
-    hipLaunchKernelGGL((welch_dif_kernel<N, true>), grid, block, lds, st, (const v2f *)x, len, win,
-                       (const v2f *)tw, g, rows, frames);
-  else
-    hipLaunchKernelGGL((welch_dif_kernel<N, false>), grid, block, lds, st, (const v2f *)x, len, win,
-                       (const v2f *)tw, g, rows, frames);
+#define WELCH_DIF_GO(P, H)                                                                          \
+  hipLaunchKernelGGL((welch_dif_kernel<N, P, H>), grid, block, lds, st, (const v2f *)x, len, win, \
+                     (const v2f *)tw, g, rows, frames)
+  if (prune) {
+    if (half) WELCH_DIF_GO(true, true);
+    else WELCH_DIF_GO(true, false);
+  } else {
+    if (half) WELCH_DIF_GO(false, true);
+    else WELCH_DIF_GO(false, false);
+  }
+#undef WELCH_DIF_GO
   if (g.split > 1) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
