@@ -934,6 +934,7 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
     const PcEdgeConst &m1 = K == 2 ? kPcEdge4Idx[1 + (L & 3)] : kPcEdgeIdx[1 + (L & 7)];
     const float *const V[2] = {eb + m0.v, eb + m1.v};
     const int J[2] = {m0.J, m1.J}, r[2] = {m0.r, m1.r};
+    // submitted after the walk's launch (before it: the same step time, profiles/r06r)
     e = launch_pc_edge_v(in, p->lo.as<float2>(), p->edge_v.as<float2>(), frames, V, J, r, p->side_st);
     if (e != hipSuccess) return hip_fail(e, "pc_edge_v launch");
   } else {
