@@ -292,40 +292,35 @@ class ZoomFFT:
               "zfft_waterfall_render")
         return out
 
-    def _slot(self, attr: str, shape, dtype):
-        """One of two page-locked buffers this plan owns for `attr`, used in turn."""
-        slots = getattr(self, attr, None)
-        if not slots or slots[0].shape != shape or slots[0].dtype != dtype:
-            slots = [pinned_empty(shape, dtype) for _ in range(2)]
-            setattr(self, attr, slots)
-            setattr(self, attr + "_k", 0)
-        k = getattr(self, attr + "_k")
-        setattr(self, attr + "_k", k + 1)
-        return slots[k % 2]
-
     def waterfall_push_emit(self, rows, f64: bool, out: np.ndarray | None = None) -> np.ndarray:
         """`rows` ((count, n_win) float32 host rows, or None) pushed, then the image in one
         round trip (zfft_waterfall_push_render / _push_read64): RGBA uint8 (H, W, 4), or the
         float64 (H, W) image when `f64`.  Without `out` the image lands in one of two
         page-locked buffers the engine owns and uses in turn, valid until the call after next
-        (as waterfall_render); pass `out` to keep one."""
-        hw = getattr(self, "_wf_hw", None)  # fixed per plan (n_win / 4 x n_win)
-        if hw is None:
-            hw = self._wf_hw = self.waterfall_shape()
-        h, w = hw
-        shape, dtype = ((h, w), np.float64) if f64 else ((h, w, 4), np.uint8)
+        (as waterfall_render); pass `out` to keep one.  (The per-line display path: kept to a
+        few attribute reads and two integer pointers on the Python side.)"""
+        st = self.__dict__.get("_emit_state")
+        if st is None:
+            h, w = self.waterfall_shape()  # fixed per plan (n_win / 4 x n_win)
+            st = self._emit_state = {
+                True: [[pinned_empty((h, w), np.float64) for _ in range(2)], 0, (h, w), np.float64,
+                       self.lib.zfft_waterfall_push_read64, "zfft_waterfall_push_read64"],
+                False: [[pinned_empty((h, w, 4), np.uint8) for _ in range(2)], 0, (h, w, 4), np.uint8,
+                        self.lib.zfft_waterfall_push_render, "zfft_waterfall_push_render"],
+                "w": w}
+        slot = st[bool(f64)]
         if out is None:
-            out = self._slot("_img64_slots" if f64 else "_render_slots2", shape, dtype)
-        elif out.shape != shape or out.dtype != dtype or not out.flags.c_contiguous:
-            raise ValueError(f"out must be a C-contiguous {np.dtype(dtype).name} array of shape {shape}")
+            out = slot[0][slot[1] & 1]
+            slot[1] += 1
+        elif out.shape != slot[2] or out.dtype != slot[3] or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous {np.dtype(slot[3]).name} array of shape {slot[2]}")
         if rows is None:
             count, ptr = 0, None
         else:
-            r = np.ascontiguousarray(rows, dtype=np.float32).reshape(-1, w)
-            count, ptr = r.shape[0], r.ctypes.data_as(ctypes.c_void_p)
-        fn = self.lib.zfft_waterfall_push_read64 if f64 else self.lib.zfft_waterfall_push_render
-        check(fn(self._plan, ptr, count, out.ctypes.data_as(ctypes.c_void_p)),
-              "zfft_waterfall_push_read64" if f64 else "zfft_waterfall_push_render")
+            r = rows if (rows.dtype == np.float32 and rows.flags.c_contiguous) else \
+                np.ascontiguousarray(rows, dtype=np.float32)
+            count, ptr = r.size // st["w"], r.ctypes.data
+        check(slot[4](self._plan, ptr, count, out.ctypes.data), slot[5])
         return out
 
     def waterfall_render_device(self, d_rgba_ptr: int, stream: int = 0) -> None:
