@@ -9,9 +9,9 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libzfft.so")
-SOURCES = ["zfft_kernels.hip", "xa_kernels.hip", "pc_kernels.hip", "zfft_plan.cpp",
+SOURCES = ["zfft_kernels.hip", "xa_kernels.hip", "pc_kernels.hip", "fc_kernels.hip", "zfft_plan.cpp",
            "pc_tables.cpp", "zfft_ring.cpp", "windows.cpp"]
-HEADERS = ["zfft_internal.h", "zfft_device.h", "cheby1_q2.h", "pc_edge_maps.h", os.path.join("..", "..", "include", "zfft.h")]
+HEADERS = ["zfft_internal.h", "zfft_device.h", "zfft_fft.h", "zfft_pairs.h", "cheby1_q2.h", "pc_edge_maps.h", os.path.join("..", "..", "include", "zfft.h")]
 ARCH = os.environ.get("ZFFT_OFFLOAD_ARCH", "gfx950")
 
 

@@ -1,0 +1,342 @@
+// fc_kernels.hip -- "FC", the fast-convolution form of the zoom-8 decimator on gfx950 (host
+// tables: fc_build_table in pc_tables.cpp; design model: tools/fc_model.py).
+//
+// The interior of three scipy.signal.decimate(x, 2) (pypanadapter_spectrum.py:2096-2098) is the
+// zero-phase LTI filter G = prod_k |H(z^(2^k))|^2 on the zero-extended frame followed by [::8]
+// (DESIGN §3.5).  Its input-rate impulse response g falls below 1.5e-8 of sum |g| beyond
+// |k| = kFcK = 1024 (tools/fc_model.py); truncated there it is applied by overlap-save FFT
+// convolution, one 8192-sample window per block:
+//   block b: window w[n] = x[6144 b - 1024 + n], n < 8192 (zero outside the frame)
+//   residues a_r[m] = w[8m + r]: eight 1024-point DFTs A_r (radix 16, 16, 4; decimation in
+//            frequency, in lock step: the residues share every twiddle)
+//   Yf[k] = sum_r A_r[k] C[k][r],  C[k][r] = W_8192^(rk) sum_q G[k + 1024 q] W_8^(rq) / 8192
+//            -- the [::8] is an alias sum in frequency, here fused with the filter
+//   y[j] = IDFT_1024(Yf)[j] (five radix-4 stages), outputs m = 768 b + j - 128, j in [128, 896)
+// The LO mix moves into the filter: (x lo) * g at 8m equals lo[8m] (x * g') with
+// g'[k] = g[k] e^(2 pi i f_lo k / fs) (lo[n] = sqrt 2 e^(-2 pi i f_lo n / fs) is an exact
+// exponential), so C holds the modulated filter's spectrum (one table per LO row) and each output
+// takes lo[8m] once, as the composite lo[6144 b] lo[8 (j - 128)] / sqrt 2.
+// Frame ends: the walk's maps (pc_edge_v beside this kernel on the side stream, pc_edge_u after
+// the join: exact minus the zero-extended model), which g's truncation changes by < 2e-8.
+//
+// Work per input sample: ~30 VALU lane-instructions (the walk: 74); LDS: two
+// exchanges of the 8192-point window plus five small ones of the 1024-point inverse per block.
+#include <algorithm>
+
+#include "zfft_device.h"
+#include "zfft_fft.h"
+#include "zfft_pairs.h"
+
+namespace zfft {
+namespace fc {
+
+typedef v2f __attribute__((address_space(3))) *LP;
+typedef v4f __attribute__((address_space(3))) *LP4;
+
+constexpr int kN = kFcN, kM = kFcN / 8;  // window, per-residue transform
+constexpr int kS = kFcStep;              // 512-sample chunks a block advances
+constexpr int kK = kFcK;                 // half length of the truncated response
+constexpr int kP = kFcP;                 // outputs per block
+constexpr int kKeep = 16 - kS;           // a thread's pairs carried into the next window
+constexpr int kJ0 = kK / 8;              // first valid inverse output
+static_assert(kK == (kN - 512 * kS) / 2 && kP == 64 * kS && kK % 8 == 0, "FC block geometry");
+// LDS: the window as [pos][residue] with 2 pad slots per 32 (conflict-free b128 reads in all
+// three forward passes, tools/fc_model.py layout check); the inverse 1024 points, 1 pad per 16
+constexpr int kBigSlots = kN + 2 * (kN / 32);
+constexpr int kSmallSlots = kM + kM / 16;
+__device__ __forceinline__ int pb(int i) { return i + 2 * (i >> 5); }
+__device__ __forceinline__ int ps(int i) { return i + (i >> 4); }
+
+// acc + a b (complex) in two VOP3P instructions (cmul2 with the accumulator as the addend)
+__device__ __forceinline__ v2f cmac2(v2f acc, v2f a, v2f b) {
+  v2f t, r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(a), "v"(b), "v"(acc));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+__device__ __forceinline__ v2f conj(v2f a) { return v2f{a.x, -a.y}; }
+// sum_a v_a W_4^(-ab): the forward radix 4 with outputs 1 and 3 exchanged
+__device__ __forceinline__ void idft4(v2f *v) {
+  dft<4>(v);
+  const v2f s = v[1];
+  v[1] = v[3];
+  v[3] = s;
+}
+// v[b] *= w^b, b = 1..3
+__device__ __forceinline__ void pow_tw3(v2f *v, v2f w) {
+  const v2f w2 = cmul2(w, w);
+  v[1] = cmul2(v[1], w);
+  v[2] = cmul2(v[2], w2);
+  v[3] = cmul2(v[3], cmul2(w2, w));
+}
+
+// Loads through buffer resources: one lane offset VGPR and constant SGPR offsets per load (64-bit
+// addresses per load, hoisted out of the block loop, spilled 60-100 VGPRs), and a load past the
+// resource's end returns 0 (the window's samples outside the frame).
+constexpr int kBufFlags = 0x00020000;
+template <int DT>
+constexpr int ebytes() { return DT == kInC64 ? 8 : DT == kInCU8 ? 2 : 4; }
+template <int DT>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const InDesc &in, int64_t f) {
+  constexpr int eb = ebytes<DT>();
+  return __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)in.p + f * in.stride * eb), (short)0,
+                                           (int)(in.len * eb), kBufFlags);
+}
+// sample n of the frame (0 outside it)
+template <int DT, int FLIP>
+__device__ __forceinline__ v2f load_sample(__amdgpu_buffer_rsrc_t rs, int64_t L, int64_t n) {
+  constexpr int eb = ebytes<DT>();
+  const int64_t k = FLIP ? L - 1 - n : n;
+  const uint32_t vo = n >= 0 && n < L ? (uint32_t)(k * eb) : 0x80000000u;
+  if constexpr (DT == kInC64) {
+    return __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, 0, 0));
+  } else if constexpr (DT == kInC32H) {
+    const h2 h = __builtin_bit_cast(h2, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0));
+    return v2f{(float)h.x, (float)h.y};
+  } else if constexpr (DT == kInF32R) {
+    return v2f{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0)), 0.f};
+  } else {
+    const u8x2 u = __builtin_bit_cast(u8x2, __builtin_amdgcn_raw_buffer_load_b16(rs, vo, 0, 0));
+    return v2f{((float)u.x - 127.5f) * (1.f / 127.5f), ((float)u.y - 127.5f) * (1.f / 127.5f)};
+  }
+}
+// the raw pair (n, n + 1), n = s + 2t + 512 j, of a window inside the frame: voffset from
+// pair_vo (per block), soffset the constant 512 eb j (mirrored for FLIP)
+template <int DT, int FLIP>
+__device__ __forceinline__ uint32_t pair_vo(int64_t L, int64_t s, int t) {
+  constexpr int eb = ebytes<DT>();
+  return (uint32_t)((FLIP ? L - 2 - s - 7680 - 2 * t : s + 2 * t) * eb);
+}
+template <int DT, int FLIP>
+__device__ __forceinline__ typename RawP<DT>::T load_pair_b(__amdgpu_buffer_rsrc_t rs, uint32_t vo, int j) {
+  constexpr int eb = ebytes<DT>();
+  const int so = 512 * eb * (FLIP ? 15 - j : j);
+  typedef typename RawP<DT>::T T;
+  if constexpr (DT == kInC64) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
+  else if constexpr (DT == kInCU8) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0));
+  else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
+}
+
+// One workgroup walks blocks [bpc * blockIdx.x, +bpc) of frame blockIdx.y.  tab: W_1024^k
+// (k < 1024), then per LO row (row_stride apart) C as v4f pairs [4 k3 + r / 2][t] (r, r + 1) for
+// thread t of pass C.  Needs frames of >= kFcN samples and < 2^31 bytes (launch_fc_decim).
+template <int DT, int FLIP>
+__global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *lo, const v2f *tab,
+                                                         int64_t row_stride, v2f *out, int64_t n3,
+                                                         int bpc) {
+  __shared__ v4f big4[kBigSlots / 2];
+  __shared__ v2f small_[kSmallSlots];
+  const LP bl = (LP)big4;
+  const LP sl = (LP)small_;
+  const int t = threadIdx.x;
+  const int64_t f = blockIdx.y, L = in.len;
+  const int nb = (int)((n3 + kP - 1) / kP);
+  const int b0 = (int)blockIdx.x * bpc, b1 = min(nb, b0 + bpc);
+  if (b0 >= b1) return;
+  const v2f *lor = lo_row(lo, in, f);
+  const int row = in.lo_n <= 1 ? 0 : (int)((((int64_t)in.lo_first + f) / in.lo_per) % in.lo_n);
+  const v2f *tw = tab;
+  const __amdgpu_buffer_rsrc_t crs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(tab + kM + row * row_stride), (short)0, kFcRow * 8, kBufFlags);
+  const __amdgpu_buffer_rsrc_t xrs = frame_rsrc<DT>(in, f);
+  // pass A: j0 = t >> 2 (residues 2 (t & 3), +1); pass B: k1 = t >> 4, j1 = (t >> 2) & 3
+  v2f bA[4], bB[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    bA[s] = tw[((t >> 2) << s) & (kM - 1)];
+    bB[s] = tw[((16 * ((t >> 2) & 3)) << s) & (kM - 1)];
+  }
+  // pass C: k1 = t >> 4, k2 = t & 15 -> kp = k1 + 16 k2
+  const int kp = (t >> 4) + 16 * (t & 15);
+  // inverse twiddle bases, conjugated: stage 1 W^kp, 2 W^(4 (t & 63)), 3 W^(16 (t & 15)),
+  // 4 W^(64 (t & 3)) (the digits below each stage's)
+  const v2f ib0 = conj(tw[kp]), ib1 = conj(tw[4 * (t & 63)]), ib2 = conj(tw[16 * (t & 15)]),
+            ib3 = conj(tw[64 * (t & 3)]);
+  // outputs: j = t + 256 b4; the three valid j in [128, 896) are jm = j - 128 =
+  // ((t + 128) & 255) + 256 q, q < 3, at b4 = q + (t < 128); their lo[8 jm] (in the frame)
+  const int jm0 = (t + 128) & 255, bq = t < 128 ? 1 : 0;
+  v2f lj[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int64_t jm = jm0 + 256 * q;
+    lj[q] = jm < n3 ? lor[8 * jm] : splat(0.f);
+  }
+  // LDS bases (v2f slots; the pads of pb / ps folded into the constant strides)
+  const int aA = 2 * t + 2 * (t >> 4);                 // pb(512 k + 2t) = aA + 544 k
+  const int aB = 2 * (t & 15) + 544 * (t >> 4);        // pb(base + 32 i) = aB + 34 i
+  const int aC = 544 * (t >> 4) + 34 * (t & 15);       // pb(.. + 8 j + 2 rp) = aC + 8 j + 2 rp
+  const int a1 = kp + (kp >> 4);                       // ps(kp + 256 q) = a1 + 272 q
+  const int i2 = (t & 63) + 256 * (t >> 6), a2 = i2 + (i2 >> 4);                          // + 68 a
+  const int i3 = (t & 15) + 64 * ((t >> 4) & 3) + 256 * (t >> 6), a3 = i3 + (i3 >> 4);   // + 17 a
+  const int i4 = (t & 3) + 16 * ((t >> 2) & 3) + 64 * ((t >> 4) & 3) + 256 * (t >> 6);
+  const int a4 = i4 + (i4 >> 4);                                                         // + 4 a
+  const int i5 = 4 * (t >> 6) + 16 * ((t >> 4) & 3) + 64 * ((t >> 2) & 3) + 256 * (t & 3);
+  const int a5 = i5 + (i5 >> 4);                                                          // + a
+
+  auto wstart = [&](int b) -> int64_t { return (int64_t)(512 * kS) * b - kK; };
+  auto inside = [&](int b) { const int64_t s = wstart(b); return s >= 0 && s + kN <= L; };
+  typename RawP<DT>::T pf[kS];  // the next window's pairs kKeep .. 15
+  v2f ka[kKeep], kb[kKeep];     // this window's pairs kS .. 15 = the next window's 0 .. kKeep-1
+  bool carried = false;         // ka, kb and pf hold this block's window
+  for (int b = b0; b < b1; ++b) {
+    v2f xa[16], xb[16];
+    // this block's lo[6144 b], requested before the prefetch: its wait at the outputs then
+    // leaves the prefetch in flight (the vector-memory counter completes in order)
+    const int64_t m0 = (int64_t)kP * b;
+    const v2f lob = lor[8 * m0];
+    {
+      const int64_t s = wstart(b);
+      if (carried) {
+#pragma unroll
+        for (int i = 0; i < kKeep; ++i) {
+          xa[i] = ka[i];
+          xb[i] = kb[i];
+        }
+#pragma unroll
+        for (int i = 0; i < kS; ++i) cvt_pair<DT, FLIP>(pf[i], xa[kKeep + i], xb[kKeep + i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int64_t n = s + 2 * t + 512 * i;
+          xa[i] = load_sample<DT, FLIP>(xrs, L, n);
+          xb[i] = load_sample<DT, FLIP>(xrs, L, n + 1);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kKeep; ++i) {
+        ka[i] = xa[kS + i];
+        kb[i] = xb[kS + i];
+      }
+      // the next window's new pairs, issued on every block from a window start clamped into
+      // the frame (values unused when the next window is not inside it): one unconditional
+      // call site, so the wait before their use counts only what was issued after them
+      carried = b + 1 < b1 && inside(b + 1);
+      int64_t sn = wstart(b + 1);
+      sn = sn < 0 ? 0 : (sn > L - kN ? L - kN : sn);
+      const uint32_t vo = pair_vo<DT, FLIP>(L, sn, t);
+#pragma unroll
+      for (int i = 0; i < kS; ++i) pf[i] = load_pair_b<DT, FLIP>(xrs, vo, kKeep + i);
+    }
+    // pass A: DFT16 over i (m = j0 + 64 i) -> k1, twiddle W_1024^(j0 k1), to LDS at (64 k1 + j0, r)
+    dft<16>(xa);
+    apply_powers(xa, bA);
+    dft<16>(xb);
+    apply_powers(xb, bA);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) *(LP4)(bl + aA + 544 * k) = cat(xa[k], xb[k]);
+    __syncthreads();
+    // pass B: (64 k1 + j1 + 4 i2) -> DFT16 over i2 -> k2, twiddle W_64^(j1 k2), in place
+    {
+      v2f ya[16], yb[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const v4f w = *(LP4)(bl + aB + 34 * i);
+        ya[i] = lo2(w);
+        yb[i] = hi2(w);
+      }
+      dft<16>(ya);
+      apply_powers(ya, bB);
+      dft<16>(yb);
+      apply_powers(yb, bB);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) *(LP4)(bl + aB + 34 * k) = cat(ya[k], yb[k]);
+    }
+    __syncthreads();
+    // pass C: (64 k1 + 4 k2 + j1, r) for all j1, r -> DFT4 over j1 -> k3; Yf = sum_r A_r C;
+    // inverse stage 1 (radix 4 over k3 -> b0, twiddle W_1024^(-b0 kp)) to (kp + 256 b0)
+    {
+      v4f cr[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        cr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(crs, (uint32_t)(16 * t), 4096 * i, 0));
+      // one residue pair at a time: its four j1 values, DFT4 each, accumulated into Yf (the
+      // whole window's 32 values and C's 32 at once spilled)
+      v2f yf[4] = {splat(0.f), splat(0.f), splat(0.f), splat(0.f)};
+#pragma unroll
+      for (int rp = 0; rp < 4; ++rp) {
+        v2f ea[4], eb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const v4f w = *(LP4)(bl + aC + 8 * j + 2 * rp);
+          ea[j] = lo2(w);
+          eb[j] = hi2(w);
+        }
+        dft<4>(ea);
+        dft<4>(eb);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const v4f c = cr[4 * k + rp];
+          yf[k] = cmac2(cmac2(yf[k], ea[k], lo2(c)), eb[k], hi2(c));
+        }
+      }
+      idft4(yf);
+      pow_tw3(yf, ib0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sl[a1 + 272 * q] = yf[q];
+    }
+    __syncthreads();
+    // inverse stages 2..4: radix 4 over the digit at stride S, twiddle W_(4S)^(-b k_low)
+    auto istage = [&](int a0, int st, v2f w) {
+      v2f v[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) v[a] = sl[a0 + st * a];
+      idft4(v);
+      pow_tw3(v, w);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) sl[a0 + st * a] = v[a];
+    };
+    istage(a2, 68, ib1);
+    __syncthreads();
+    istage(a3, 17, ib2);
+    __syncthreads();
+    istage(a4, 4, ib3);
+    __syncthreads();
+    // stage 5: t = b0 + 4 b1 + 16 b2 + 64 b3 reads (a0 + 4 b3 + 16 b2 + 64 b1 + 256 b0) -> b4
+    {
+      v2f v[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) v[a] = sl[a5 + a];
+      idft4(v);
+      v2f *o = out + f * n3 + m0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int64_t jm = jm0 + 256 * q;
+        const v2f y = bq ? v[q + 1] : v[q];
+        if (m0 + jm < n3) o[jm] = cmul2(y, cmul2(lob, lj[q]));
+      }
+    }
+  }
+}
+
+}  // namespace fc
+
+hipError_t launch_fc_decim(const InDesc &in, const float2 *lo, const float2 *tab, int64_t row_stride,
+                           float2 *out, int64_t n3, int frames, hipStream_t st) {
+  if (in.len < kFcN || in.len * (int64_t)in_elem_bytes(in.dtype) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  const int nb = (int)((n3 + kFcP - 1) / kFcP);
+  // about two rounds of the chip's 512 resident workgroups: whole frames from 1024 frames per
+  // call, below that each frame split into runs of blocks (a run's first window loads in full)
+  const int chunks = std::max(1, std::min(nb, (1024 + frames - 1) / frames));
+  const int bpc = (nb + chunks - 1) / chunks;
+  const dim3 grid((unsigned)((nb + bpc - 1) / bpc), (unsigned)frames);
+  const v2f *l = (const v2f *)lo, *tb = (const v2f *)tab;
+  v2f *o = (v2f *)out;
+#define FC_GO(DT, FL) \
+  hipLaunchKernelGGL((fc::fc_decim_kernel<DT, FL>), grid, dim3(256), 0, st, in, l, tb, row_stride, o, n3, bpc)
+  if (in.flip) {
+    if (in.dtype == kInC64) FC_GO(kInC64, 1);
+    else if (in.dtype == kInC32H) FC_GO(kInC32H, 1);
+    else if (in.dtype == kInCU8) FC_GO(kInCU8, 1);
+    else FC_GO(kInF32R, 1);
+  } else {
+    if (in.dtype == kInC64) FC_GO(kInC64, 0);
+    else if (in.dtype == kInC32H) FC_GO(kInC32H, 0);
+    else if (in.dtype == kInCU8) FC_GO(kInCU8, 0);
+    else FC_GO(kInF32R, 0);
+  }
+#undef FC_GO
+  return hipGetLastError();
+}
+
+}  // namespace zfft

@@ -387,6 +387,47 @@ bool pc_build_tables2(PcTab2 &tab) {
 
 bool pc_edge_map(int side, int lmod8, PcEdge &out) { return pc_edge_map_k(3, side, lmod8, out); }
 
+// ---- FC tables (fc_kernels.hip; tools/fc_model.py c_table) ----
+
+void fc_build_twiddles(float2 *tw) {
+  for (int k = 0; k < kFcN / 8; ++k) {
+    const double a = -2.0 * M_PI * k / (kFcN / 8);
+    tw[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+}
+
+// g'[k] = g[k] e^(2 pi i lo_ratio k), |k| <= kFcK (g = the zoom-8 model's input-rate response,
+// model_hz(3)), placed circularly in kFcN; G = its DFT; C[k][r] = W_N^(rk) sum_q G[k + M q] W_8^(rq)
+// / (N sqrt 2) for k < M = N / 8 (the 1 / sqrt 2: the outputs take lo[8m] as the composite
+// lo[a] lo[b] = sqrt 2 lo[a + b]).  Stored for pass C's thread t (k' = (t >> 4) + 16 (t & 15)):
+// row as v4f pairs: float2 index ((4 k3 + r / 2) 256 + t) 2 + r % 2 holds C[k' + 256 k3][r].
+bool fc_build_row(double lo_ratio, float2 *row) {
+  constexpr int N = kFcN, M = kFcN / 8;
+  const std::vector<double> &h = model_hz(kPcStages);
+  if ((int)h.size() < 2 * kFcK + 1) return false;
+  const int hc = ((int)h.size() - 1) / 2;
+  std::vector<std::complex<double>> g(N, 0.0);
+  for (int k = -kFcK; k <= kFcK; ++k) {
+    const double turns = std::fmod(lo_ratio * (double)k, 1.0);
+    g[(k + N) % N] = h[hc + k] * std::polar(1.0, 2.0 * M_PI * turns);
+  }
+  fft_inplace(g, false);
+  const double s = 1.0 / ((double)N * std::sqrt(2.0));
+  for (int t = 0; t < 256; ++t) {
+    const int kp = (t >> 4) + 16 * (t & 15);
+    for (int k3 = 0; k3 < 4; ++k3) {
+      const int k = kp + 256 * k3;
+      for (int r = 0; r < 8; ++r) {
+        std::complex<double> c = 0.0;
+        for (int q = 0; q < 8; ++q) c += g[k + M * q] * std::polar(1.0, -2.0 * M_PI * ((r * q) % 8) / 8.0);
+        c *= std::polar(s, -2.0 * M_PI * (double)((int64_t)r * k % N) / N);
+        row[((4 * k3 + r / 2) * 256 + t) * 2 + (r & 1)] = make_float2((float)c.real(), (float)c.imag());
+      }
+    }
+  }
+  return true;
+}
+
 bool pc_edge_map_k(int K, int side, int lmod, PcEdge &out) {
   const int R = kPcEdgeR, J = side == 0 ? 768 : kPcEdgeJ;
   std::vector<double> C;
@@ -472,9 +513,17 @@ bool pc_edge_map_k(int K, int side, int lmod, PcEdge &out) {
 //   5: zoom 4 FIR taps g0 | g1 (74 floats); 12 / 13: zoom-4 left / right map for L mod 4 = arg
 //   built now; 14: the shipped zoom-4 map arg; 6: zoom 2 FIR taps M + its input-rate and
 //   output-rate sections' a1, a2 (41 floats); 15 / 16: zoom-2 left / right map for L mod 2 = arg
-//   built now; 17: the shipped zoom-2 map arg.
+//   built now; 17: the shipped zoom-2 map arg; 18: the FC twiddles W_1024^k (2048 floats);
+//   19: the FC filter row for f_lo / fs = arg / 2^20 (kFcRow complex as floats, kernel order).
 extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
   using namespace zfft;
+  if (what == 18 || what == 19) {
+    const int n = what == 18 ? 2 * (kFcN / 8) : 2 * kFcRow;
+    if (cap < n) return -2;
+    if (what == 18) fc_build_twiddles((float2 *)out);
+    else if (!fc_build_row((double)arg / (double)(1 << 20), (float2 *)out)) return -1;
+    return n;
+  }
   if (what == 0 || what == 1) {
     PcTab t;
     if (!pc_build_tables(t)) return -1;

@@ -266,6 +266,19 @@ hipError_t launch_pc_edge_u(const float2 *v, float2 *out, int64_t n3, int frames
 hipError_t launch_pc_edge(const InDesc &in, const float2 *lo, float2 *out, int64_t n3, int frames,
                           const float *const U[2], const float *const V[2], const int R[2],
                           const int J[2], const int r[2], hipStream_t st);
+// FC (fc_kernels.hip, path 6): the zoom-8 model G as a truncated FIR (|k| <= kFcK) applied by
+// overlap-save FFT convolution in 8192-sample windows advancing 512 kFcStep samples (kFcP
+// outputs); the ↓8 is an alias sum in frequency fused with the filter, the LO mix is the
+// filter's modulation.  The table: W_1024^k (k < 1024), then kFcRow entries per LO row.
+constexpr int kFcN = 8192, kFcStep = 12;
+constexpr int kFcK = (kFcN - 512 * kFcStep) / 2;   // 1024
+constexpr int kFcP = 64 * kFcStep;                 // 768
+constexpr int kFcRow = kFcN;                       // C[k][r] per LO row, [4 k3 + r/2][t] (r, r+1) pairs
+// C for LO frequency ratio f_lo / fs into row (kFcRow entries); false if the model is unavailable
+bool fc_build_row(double lo_ratio, float2 *row);
+void fc_build_twiddles(float2 *tw);                // W_1024^k, k < 1024
+hipError_t launch_fc_decim(const InDesc &in, const float2 *lo, const float2 *tab, int64_t row_stride,
+                           float2 *out, int64_t n3, int frames, hipStream_t st);
 
 struct WelchGeom {
   int n_fft, log2n;

@@ -433,6 +433,10 @@ struct zfft_plan {
   hipStream_t side_st = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   DevBuf edge_v;
+  // FC decimator (path 6): W_1024 twiddles, then one C row per LO frequency; fc_built holds the
+  // f_lo / fs ratios the rows were built for (rebuilt when they change)
+  DevBuf fc_tab;
+  std::vector<double> fc_built;
 };
 
 namespace {
@@ -890,13 +894,43 @@ int ensure_pc(zfft_plan *p) {
   return ZFFT_OK;
 }
 
+// FC tables for the plan's LO rows (host fp64 build, fc_build_row; one synchronous upload when
+// the LO frequencies change, after the plan's enqueued work)
+int ensure_fc(zfft_plan *p) {
+  const std::vector<double> freqs = p->lo_freqs.empty() ? std::vector<double>{p->cfg.f_lo} : p->lo_freqs;
+  std::vector<double> ratios;
+  for (double fr : freqs) ratios.push_back(fr / p->cfg.fs);
+  if (p->fc_tab.p && p->fc_built == ratios) return ZFFT_OK;
+  int rc = quiesce(p);
+  if (rc) return rc;
+  std::vector<float2> h;
+  try {
+    h.resize(kFcN / 8 + ratios.size() * (size_t)kFcRow);
+  } catch (const std::bad_alloc &) {
+    return fail(ZFFT_ENOMEM, "FC table host staging allocation failed");
+  }
+  fc_build_twiddles(h.data());
+  for (size_t k = 0; k < ratios.size(); ++k)
+    if (!fc_build_row(ratios[k], h.data() + kFcN / 8 + k * kFcRow))
+      return fail(ZFFT_EINTERNAL, "FC table: model response unavailable");
+  hipError_t e = p->fc_tab.ensure(h.size() * sizeof(float2));
+  if (e != hipSuccess) return fail(ZFFT_ENOMEM, "FC table allocation failed");
+  e = hipMemcpy(p->fc_tab.p, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "FC table upload");
+  p->fc_built = ratios;
+  return ZFFT_OK;
+}
+
 // PC path: K1 (FIRs) -> y2 (ping) -> K2 (own-rate sections, FIR, output-rate sections) ->
 // out (pong) -> K3 (frame-end maps, in place).
 // K = the stages PC runs: p->K (zoom 4 or 8), or 3 as the head of a longer cascade.
+// fc (zoom 8, K = 3, with walk): the FC kernel in the walk's place (fc_kernels.hip, path 6).
 int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vector<int64_t> &n,
-           bool walk, const float2 **out, hipStream_t st, int K) {
+           bool walk, const float2 **out, hipStream_t st, int K, bool fc = false) {
   int rc = ensure_pc(p);
   if (rc) return rc;
+  fc = fc && walk && K == kPcStages;
+  if (fc && (rc = ensure_fc(p))) return rc;
   const int64_t n3 = n[K];
   const PcTab *tab = p->pc_tab.as<PcTab>();
   hipError_t e;
@@ -925,10 +959,11 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
     e = hipEventRecord(p->fork_ev, st);
     if (e == hipSuccess) e = hipStreamWaitEvent(p->side_st, p->fork_ev, 0);
     if (e != hipSuccess) return hip_fail(e, "side stream fork");
-    if (K == 2) e = launch_pc_walk4(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab4.as<PcTab4>(), st);
+    if (fc) e = launch_fc_decim(in, p->lo.as<float2>(), p->fc_tab.as<float2>(), kFcRow, p->pong.as<float2>(), n3, frames, st);
+    else if (K == 2) e = launch_pc_walk4(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab4.as<PcTab4>(), st);
     else e = launch_pc_walk(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, tab, st);
-    if (e != hipSuccess) return hip_fail(e, "pc_walk launch");
-    mark(p, st, K == 2 ? "pc_walk4" : "pc_walk");
+    if (e != hipSuccess) return hip_fail(e, fc ? "fc_decim launch" : "pc_walk launch");
+    mark(p, st, fc ? "fc_decim" : K == 2 ? "pc_walk4" : "pc_walk");
     const float *eb = p->pc_edge.as<float>();
     const PcEdgeConst &m0 = K == 2 ? kPcEdge4Idx[0] : kPcEdgeIdx[0];
     const PcEdgeConst &m1 = K == 2 ? kPcEdge4Idx[1 + (L & 3)] : kPcEdgeIdx[1 + (L & 7)];
@@ -1047,27 +1082,27 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   // blocked schedules split each frame over many waves and win for a few frames per call
   const bool pc8 = pc_fits(p, L, frames), head = pc_head_fits(p, L, frames), pc4 = pc4_fits(p, L, frames),
              pc2 = pc2_fits(p, L, frames);
-  if ((p->path == 4 || p->path == 5) && !pc8 && !head && !pc4 && !pc2)
+  if (p->path >= 4 && !pc8 && !head && !pc4 && !pc2)
     return fail(ZFFT_EUNSUPPORTED, "PC decimator needs frames of >= 16384 samples and <= 65535 "
                                    "frames per call");
   // the tiles hand a batch over to XA only where XA takes it (auto_xa: from 768 frames of
   // > 2^19 samples), never to the blocked passes, which lose to the tiles at every batch
   const bool xa_auto = auto_xa(frames, L) && xa_fits(p, L);
   // zoom 2: the tiles on request (paths 4, 5) and automatic below 512 frames per call
-  if (pc2 && (p->path == 4 || p->path == 5 || (p->path == 0 && (frames < kPc2TilesMaxFrames || !xa_auto))))
+  if (pc2 && (p->path >= 4 || (p->path == 0 && (frames < kPc2TilesMaxFrames || !xa_auto))))
     return run_pc(p, in, L, frames, n, false, out, st, 1);
   // zoom 4: the tiles below 512 frames per call, the walk from there (both on request too)
-  if (pc4 && (p->path == 4 || p->path == 5 || p->path == 0))
-    return run_pc(p, in, L, frames, n, p->path == 5 || (p->path == 0 && frames >= kPc4WalkMinFrames), out,
+  if (pc4 && (p->path >= 4 || p->path == 0))
+    return run_pc(p, in, L, frames, n, p->path >= 5 || (p->path == 0 && frames >= kPc4WalkMinFrames), out,
                   st, p->K);
-  const bool walk = p->path == 5 || (p->path == 0 && frames >= kPcWalkMinFrames);
+  const bool walk = p->path >= 5 || (p->path == 0 && frames >= kPcWalkMinFrames);
   // PC is the fastest schedule wherever it applies, from one frame per call (the
   // reference's use: 0.083 against 0.37 ms for path 1) to full batches (1024 frames: 1.44
   // against 2.03 ms for XA) -- tools/sweep_schedule.py, profiles/r04l
-  if (pc8 && (p->path == 0 || p->path == 4 || p->path == 5))
-    return run_pc(p, in, L, frames, n, walk, out, st, p->K);
+  if (pc8 && (p->path == 0 || p->path >= 4))
+    return run_pc(p, in, L, frames, n, walk, out, st, p->K, p->path == 6);
   // zoom >= 16: the head, then XA or the blocked passes for the rest (by the tail's batch)
-  if (p->path == 4 || p->path == 5 || (p->path == 0 && head && xa_fits(p, L)))
+  if (p->path >= 4 || (p->path == 0 && head && xa_fits(p, L)))
     return run_pc_head(p, in, L, frames, n, walk, out, st);
   if (p->path == 3 || (p->path == 0 && auto_xa(frames, L) && xa_fits(p, L)))
     return run_xa(p, in, frames, n, out, st);
@@ -1354,7 +1389,7 @@ int zfft_plan_destroy(zfft_plan *p) {
                     &p->ring, &p->img, &p->one_row, &p->dec, &p->edge, &p->xk, &p->xa_tab,
                     &p->tws, &p->means, &p->z4, &p->winf, &p->pc_tab, &p->pc_edge, &p->pc_tab4,
                     &p->wparts, &p->lo1, &p->pc_tab2, &p->lut_d, &p->rgba, &p->al_hist, &p->al_bins,
-                    &p->edge_v, &p->img64})
+                    &p->edge_v, &p->img64, &p->fc_tab})
     b->release();
   if (p->row_pin) (void)hipHostFree(p->row_pin);
   for (hipEvent_t ev : p->events) (void)hipEventDestroy(ev);
@@ -1399,9 +1434,9 @@ int zfft_plan_timing(zfft_plan *p, int32_t enable) {
 }
 
 int zfft_plan_path(zfft_plan *p, int32_t path) {
-  if (!p || path < 0 || path > 5)
+  if (!p || path < 0 || path > 6)
     return fail(ZFFT_EINVAL, "path must be 0 (auto), 1 (exact), 2 (fused), 3 (XA tiles), 4 (PC "
-                             "tiles) or 5 (PC walk)");
+                             "tiles), 5 (PC walk) or 6 (FC at zoom 8, else as 5)");
   p->path = path;
   return ZFFT_OK;
 }
