@@ -66,7 +66,7 @@ TONES = ((0.31, 1.0), (-0.57, 0.1))
 # plan launch name -> kernel-name prefix in the rocprofv3 / PMC summaries
 KERNEL_OF = {"xa_stage_mix": "xa_stage_kernel<32, true", "xa_stage": "xa_stage_kernel<32, false",
              "pc_fir": "pc_fir_kernel", "pc_tail": "pc_tail_kernel", "pc_edge": "pc_edge_kernel",
-             "pc_walk": "pc_walk_kernel",
+             "pc_walk": "pc_walk_kernel", "fc_decim": "fc_decim_kernel",
              "welch_rows": "welch_", "welch4": "welch4_"}
 
 
@@ -94,7 +94,7 @@ def own_bytes_per_frame(name: str, bps: int, L: int, zoom: int, W: int, stage: i
     if name == "pc_tail":
         y2 = ((L + 15) // 2 + 24) // 2 + 17
         return 8 * y2 + 8 * n[-1]
-    if name == "pc_walk":  # IQ in, decimated IQ out (y2 stays in LDS)
+    if name in ("pc_walk", "fc_decim"):  # IQ in, decimated IQ out (intermediates on chip)
         return bps * L + 8 * n[-1]
     if name == "pc_edge":  # ~1070 IQ samples at each end in, ~160 outputs read and written
         return bps * 2 * 1100 + 16 * 2 * 170

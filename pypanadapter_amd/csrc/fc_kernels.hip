@@ -3,19 +3,19 @@
 //
 // The interior of three scipy.signal.decimate(x, 2) (pypanadapter_spectrum.py:2096-2098) is the
 // zero-phase LTI filter G = prod_k |H(z^(2^k))|^2 on the zero-extended frame followed by [::8]
-// (DESIGN §3.5).  Its input-rate impulse response g falls below 1.5e-8 of sum |g| beyond
-// |k| = kFcK = 1024 (tools/fc_model.py); truncated there it is applied by overlap-save FFT
-// convolution, one 8192-sample window per block:
-//   block b: window w[n] = x[6144 b - 1024 + n], n < 8192 (zero outside the frame)
+// (DESIGN §3.5).  Its input-rate impulse response g falls below 1.0e-6 of sum |g| beyond
+// |k| = kFcK = 768 (1.4e-8 beyond 1024; tools/fc_model.py); truncated there it is applied by
+// overlap-save FFT convolution, one 8192-sample window per block:
+//   block b: window w[n] = x[6656 b - 768 + n], n < 8192 (zero outside the frame)
 //   residues a_r[m] = w[8m + r]: eight 1024-point DFTs A_r (radix 16, 16, 4; decimation in
 //            frequency, in lock step: the residues share every twiddle)
 //   Yf[k] = sum_r A_r[k] C[k][r],  C[k][r] = W_8192^(rk) sum_q G[k + 1024 q] W_8^(rq) / 8192
 //            -- the [::8] is an alias sum in frequency, here fused with the filter
-//   y[j] = IDFT_1024(Yf)[j] (five radix-4 stages), outputs m = 768 b + j - 128, j in [128, 896)
+//   y[j] = IDFT_1024(Yf)[j] (five radix-4 stages), outputs m = 832 b + j - 96, j in [96, 928)
 // The LO mix moves into the filter: (x lo) * g at 8m equals lo[8m] (x * g') with
 // g'[k] = g[k] e^(2 pi i f_lo k / fs) (lo[n] = sqrt 2 e^(-2 pi i f_lo n / fs) is an exact
 // exponential), so C holds the modulated filter's spectrum (one table per LO row) and each output
-// takes lo[8m] once, as the composite lo[6144 b] lo[8 (j - 128)] / sqrt 2.
+// takes lo[8m] once, as the composite lo[6656 b] lo[8 (j - 96)] / sqrt 2.
 // Frame ends: the walk's maps (pc_edge_v beside this kernel on the side stream, pc_edge_u after
 // the join: exact minus the zero-extended model), which g's truncation changes by < 2e-8.
 //
@@ -26,6 +26,22 @@
 #include "zfft_device.h"
 #include "zfft_fft.h"
 #include "zfft_pairs.h"
+
+// Diagnostic builds only (ZFFT_DIAG=1, never set by build.py), timing knockouts with wrong
+// results by design: FC_KO 1 the input loads (window values from registers), 2 the filter-table
+// loads, 4 the output stores (profiles/r06fc/r06fc4: 2.84 ms -> 1.85 / 2.61 / 2.54, all three
+// 1.56 at K = 1024).  Measured and removed: the filter table requested before the prefetch
+// (2.98 ms, spills) and the prefetch requested after the table (2.80, r06fc5).
+#ifndef ZFFT_DIAG
+#define ZFFT_DIAG 0
+#endif
+#if !ZFFT_DIAG && defined(FC_KO)
+#error "FC_KO is a diagnostic knob: build with -DZFFT_DIAG"
+#endif
+#ifndef FC_KO
+#define FC_KO 0
+#endif
+
 
 namespace zfft {
 namespace fc {
@@ -39,7 +55,8 @@ constexpr int kK = kFcK;                 // half length of the truncated respons
 constexpr int kP = kFcP;                 // outputs per block
 constexpr int kKeep = 16 - kS;           // a thread's pairs carried into the next window
 constexpr int kJ0 = kK / 8;              // first valid inverse output
-static_assert(kK == (kN - 512 * kS) / 2 && kP == 64 * kS && kK % 8 == 0, "FC block geometry");
+static_assert(kK == (kN - 512 * kS) / 2 && kP == 64 * kS && kK % 8 == 0 && kKeep >= 1, "FC block geometry");
+static_assert(kJ0 + kP <= 1024 && kJ0 < 256 && kJ0 + kP > 768, "outputs: three or four per thread");
 // LDS: the window as [pos][residue] with 2 pad slots per 32 (conflict-free b128 reads in all
 // three forward passes, tools/fc_model.py layout check); the inverse 1024 points, 1 pad per 16
 constexpr int kBigSlots = kN + 2 * (kN / 32);
@@ -83,12 +100,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const InDesc &in, i
   return __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)in.p + f * in.stride * eb), (short)0,
                                            (int)(in.len * eb), kBufFlags);
 }
-// sample n of the frame (0 outside it)
+// sample n of the frame, 0 outside it (the load returns raw 0 there, which is -1 - 1i for cu8:
+// the value is selected after the conversion)
 template <int DT, int FLIP>
 __device__ __forceinline__ v2f load_sample(__amdgpu_buffer_rsrc_t rs, int64_t L, int64_t n) {
   constexpr int eb = ebytes<DT>();
   const int64_t k = FLIP ? L - 1 - n : n;
-  const uint32_t vo = n >= 0 && n < L ? (uint32_t)(k * eb) : 0x80000000u;
+  const bool in = n >= 0 && n < L;
+  const uint32_t vo = in ? (uint32_t)(k * eb) : 0x80000000u;
   if constexpr (DT == kInC64) {
     return __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, 0, 0));
   } else if constexpr (DT == kInC32H) {
@@ -98,7 +117,8 @@ __device__ __forceinline__ v2f load_sample(__amdgpu_buffer_rsrc_t rs, int64_t L,
     return v2f{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0)), 0.f};
   } else {
     const u8x2 u = __builtin_bit_cast(u8x2, __builtin_amdgcn_raw_buffer_load_b16(rs, vo, 0, 0));
-    return v2f{((float)u.x - 127.5f) * (1.f / 127.5f), ((float)u.y - 127.5f) * (1.f / 127.5f)};
+    const v2f v{((float)u.x - 127.5f) * (1.f / 127.5f), ((float)u.y - 127.5f) * (1.f / 127.5f)};
+    return in ? v : splat(0.f);
   }
 }
 // the raw pair (n, n + 1), n = s + 2t + 512 j, of a window inside the frame: voffset from
@@ -113,9 +133,10 @@ __device__ __forceinline__ typename RawP<DT>::T load_pair_b(__amdgpu_buffer_rsrc
   constexpr int eb = ebytes<DT>();
   const int so = 512 * eb * (FLIP ? 15 - j : j);
   typedef typename RawP<DT>::T T;
-  if constexpr (DT == kInC64) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
-  else if constexpr (DT == kInCU8) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0));
-  else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
+  constexpr int aux = 2;  // non-temporal: the window is streamed once (-1 % per step, r06fc6)
+  if constexpr (DT == kInC64) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, aux));
+  else if constexpr (DT == kInCU8) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, aux));
+  else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, aux));
 }
 
 // One workgroup walks blocks [bpc * blockIdx.x, +bpc) of frame blockIdx.y.  tab: W_1024^k
@@ -153,14 +174,13 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
   // 4 W^(64 (t & 3)) (the digits below each stage's)
   const v2f ib0 = conj(tw[kp]), ib1 = conj(tw[4 * (t & 63)]), ib2 = conj(tw[16 * (t & 15)]),
             ib3 = conj(tw[64 * (t & 3)]);
-  // outputs: j = t + 256 b4; the three valid j in [128, 896) are jm = j - 128 =
-  // ((t + 128) & 255) + 256 q, q < 3, at b4 = q + (t < 128); their lo[8 jm] (in the frame)
-  const int jm0 = (t + 128) & 255, bq = t < 128 ? 1 : 0;
-  v2f lj[3];
+  // outputs: j = t + 256 b4, valid for j in [kJ0, kJ0 + kP) (three or four per thread), at
+  // output jm = j - kJ0 of the block; their lo[8 jm] (0 where invalid or past the frame)
+  v2f lj[4];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int64_t jm = jm0 + 256 * q;
-    lj[q] = jm < n3 ? lor[8 * jm] : splat(0.f);
+  for (int q = 0; q < 4; ++q) {
+    const int jm = t + 256 * q - kJ0;
+    lj[q] = jm >= 0 && jm < kP && jm < n3 ? lor[8 * jm] : splat(0.f);
   }
   // LDS bases (v2f slots; the pads of pb / ps folded into the constant strides)
   const int aA = 2 * t + 2 * (t >> 4);                 // pb(512 k + 2t) = aA + 544 k
@@ -179,15 +199,33 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
   typename RawP<DT>::T pf[kS];  // the next window's pairs kKeep .. 15
   v2f ka[kKeep], kb[kKeep];     // this window's pairs kS .. 15 = the next window's 0 .. kKeep-1
   bool carried = false;         // ka, kb and pf hold this block's window
+  // the next window's new pairs, issued on every block from a window start clamped into the
+  // frame (values unused when the next window is not inside it): one unconditional call site,
+  // so the wait before their use counts only what was issued after them
+  auto issue_pf = [&](int b) {
+    carried = b + 1 < b1 && inside(b + 1);
+    int64_t sn = wstart(b + 1);
+    sn = sn < 0 ? 0 : (sn > L - kN ? L - kN : sn);
+    const uint32_t vo = pair_vo<DT, FLIP>(L, sn, t);
+#pragma unroll
+    for (int i = 0; i < kS; ++i)
+      if (!(FC_KO & 1)) pf[i] = load_pair_b<DT, FLIP>(xrs, vo, kKeep + i);
+  };
   for (int b = b0; b < b1; ++b) {
     v2f xa[16], xb[16];
-    // this block's lo[6144 b], requested before the prefetch: its wait at the outputs then
+    // this block's lo[8 m0], requested before the prefetch: its wait at the outputs then
     // leaves the prefetch in flight (the vector-memory counter completes in order)
     const int64_t m0 = (int64_t)kP * b;
     const v2f lob = lor[8 * m0];
     {
       const int64_t s = wstart(b);
-      if (carried) {
+      if (FC_KO & 1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          xa[i] = v2f{(float)(t + i), 1.f};
+          xb[i] = v2f{1.f, (float)(t - i)};
+        }
+      } else if (carried) {
 #pragma unroll
         for (int i = 0; i < kKeep; ++i) {
           xa[i] = ka[i];
@@ -208,21 +246,12 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
         ka[i] = xa[kS + i];
         kb[i] = xb[kS + i];
       }
-      // the next window's new pairs, issued on every block from a window start clamped into
-      // the frame (values unused when the next window is not inside it): one unconditional
-      // call site, so the wait before their use counts only what was issued after them
-      carried = b + 1 < b1 && inside(b + 1);
-      int64_t sn = wstart(b + 1);
-      sn = sn < 0 ? 0 : (sn > L - kN ? L - kN : sn);
-      const uint32_t vo = pair_vo<DT, FLIP>(L, sn, t);
-#pragma unroll
-      for (int i = 0; i < kS; ++i) pf[i] = load_pair_b<DT, FLIP>(xrs, vo, kKeep + i);
+      issue_pf(b);
     }
     // pass A: DFT16 over i (m = j0 + 64 i) -> k1, twiddle W_1024^(j0 k1), to LDS at (64 k1 + j0, r)
     dft<16>(xa);
-    apply_powers(xa, bA);
     dft<16>(xb);
-    apply_powers(xb, bA);
+    apply_powers2(xa, xb, bA);
 #pragma unroll
     for (int k = 0; k < 16; ++k) *(LP4)(bl + aA + 544 * k) = cat(xa[k], xb[k]);
     __syncthreads();
@@ -236,9 +265,8 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
         yb[i] = hi2(w);
       }
       dft<16>(ya);
-      apply_powers(ya, bB);
       dft<16>(yb);
-      apply_powers(yb, bB);
+      apply_powers2(ya, yb, bB);
 #pragma unroll
       for (int k = 0; k < 16; ++k) *(LP4)(bl + aB + 34 * k) = cat(ya[k], yb[k]);
     }
@@ -249,7 +277,8 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
       v4f cr[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i)
-        cr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(crs, (uint32_t)(16 * t), 4096 * i, 0));
+        cr[i] = (FC_KO & 2) ? v4f{1.f, 0.5f, 0.25f, 1.f}
+                            : __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(crs, (uint32_t)(16 * t), 4096 * i, 0));
       // one residue pair at a time: its four j1 values, DFT4 each, accumulated into Yf (the
       // whole window's 32 values and C's 32 at once spilled)
       v2f yf[4] = {splat(0.f), splat(0.f), splat(0.f), splat(0.f)};
@@ -300,10 +329,10 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
       idft4(v);
       v2f *o = out + f * n3 + m0;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int64_t jm = jm0 + 256 * q;
-        const v2f y = bq ? v[q + 1] : v[q];
-        if (m0 + jm < n3) o[jm] = cmul2(y, cmul2(lob, lj[q]));
+      for (int q = 0; q < 4; ++q) {
+        const int jm = t + 256 * q - kJ0;
+        if (jm >= 0 && jm < kP && m0 + jm < n3 && !(FC_KO & 4))
+          __builtin_nontemporal_store(cmul2(v[q], cmul2(lob, lj[q])), o + jm);
       }
     }
   }

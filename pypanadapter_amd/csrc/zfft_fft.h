@@ -112,4 +112,30 @@ __device__ __forceinline__ void apply_powers(v2f *v, const v2f *bp) {
   v[15] = cmul2(v[15], cmul2(w7, bp[3]));
 }
 
+// apply_powers on two vectors sharing the base (the FC decimator's residue pairs): each power
+// formed once and applied to both
+__device__ __forceinline__ void apply_powers2(v2f *v, v2f *u, const v2f *bp) {
+  auto ap = [&](int i, v2f w) {
+    v[i] = cmul2(v[i], w);
+    u[i] = cmul2(u[i], w);
+  };
+  ap(1, bp[0]);
+  ap(2, bp[1]);
+  ap(4, bp[2]);
+  ap(8, bp[3]);
+  const v2f w3 = cmul2(bp[0], bp[1]), w5 = cmul2(bp[0], bp[2]), w6 = cmul2(bp[1], bp[2]);
+  const v2f w7 = cmul2(w3, bp[2]);
+  ap(3, w3);
+  ap(5, w5);
+  ap(6, w6);
+  ap(7, w7);
+  ap(9, cmul2(bp[0], bp[3]));
+  ap(10, cmul2(bp[1], bp[3]));
+  ap(11, cmul2(w3, bp[3]));
+  ap(12, cmul2(bp[2], bp[3]));
+  ap(13, cmul2(w5, bp[3]));
+  ap(14, cmul2(w6, bp[3]));
+  ap(15, cmul2(w7, bp[3]));
+}
+
 }  // namespace zfft

@@ -270,9 +270,12 @@ hipError_t launch_pc_edge(const InDesc &in, const float2 *lo, float2 *out, int64
 // overlap-save FFT convolution in 8192-sample windows advancing 512 kFcStep samples (kFcP
 // outputs); the ↓8 is an alias sum in frequency fused with the filter, the LO mix is the
 // filter's modulation.  The table: W_1024^k (k < 1024), then kFcRow entries per LO row.
-constexpr int kFcN = 8192, kFcStep = 12;
-constexpr int kFcK = (kFcN - 512 * kFcStep) / 2;   // 1024
-constexpr int kFcP = 64 * kFcStep;                 // 768
+#ifndef FC_STEP
+#define FC_STEP 13  // K = 768 (tail 1.0e-6 of sum |g|; 12 = K 1024, 1.4e-8: 5.5 % slower, r06fc6)
+#endif
+constexpr int kFcN = 8192, kFcStep = FC_STEP;
+constexpr int kFcK = (kFcN - 512 * kFcStep) / 2;   // 768
+constexpr int kFcP = 64 * kFcStep;                 // 832
 constexpr int kFcRow = kFcN;                       // C[k][r] per LO row, [4 k3 + r/2][t] (r, r+1) pairs
 // C for LO frequency ratio f_lo / fs into row (kFcRow entries); false if the model is unavailable
 bool fc_build_row(double lo_ratio, float2 *row);

@@ -809,6 +809,16 @@ constexpr int kPcWalkMinFrames = 1024;
 // 1.24 / 0.47 / 0.50, 512: 1.32 / 0.90 / 0.78, 1024: 1.69 / 1.69 / 1.44, 4096 (cfg1): 5.17 /
 // 6.27 / 4.89; profiles/r06k/sweep_walk.json).
 constexpr int kPc4WalkMinFrames = 512;
+// Zoom 8 (and the zoom >= 16 head): FC (path 6, fc_kernels.hip) from this many frames per call,
+// PC's tiles below.  ms per call, tiles / walk / FC (tools/fc_ab.py, profiles/r06fc3/fc_ab.json):
+// 299,008-sample frames 1: 0.053 / 0.39 / 0.064, 16: 0.078 / 0.41 / 0.078, 64: 0.124 / 0.41 /
+// 0.107, 512: 0.75 / 0.74 / 0.52, 4096: - / 4.69 / 3.44; 2^20-sample frames 1: 0.057 / 1.23 /
+// 0.066, 64: 0.37 / 1.30 / 0.26, 2048: - / 9.05 / 6.61.
+constexpr int kFcMinFrames = 16;
+// FC takes frames of >= kFcN samples below 2^31 bytes (its buffer loads' 32-bit offsets).
+bool fc_fits(const zfft_plan *p, int64_t L) {
+  return L >= kFcN && L * (int64_t)in_elem_bytes(p->cfg.in_dtype) < ((int64_t)1 << 31);
+}
 bool pc_fits(const zfft_plan *p, int64_t L, int frames) {
   return p->K == kPcStages && L >= kPcMinL && frames <= 65535;
 }
@@ -1010,7 +1020,7 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
 // takes the batch (ping, pong, ... in turn), else the exact blocked passes (few frames per
 // call, the reference's one: a unit LO table stands for the mix their first pass applies).
 int run_pc_head(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vector<int64_t> &n,
-                bool walk, const float2 **out, hipStream_t st) {
+                bool walk, const float2 **out, hipStream_t st, bool fc = false) {
   const float2 *cur = nullptr;
   const int64_t n3 = n[kPcStages];
   // XA where it takes the batch, except where zoom 2's tiles still beat it (< 512 frames)
@@ -1028,7 +1038,7 @@ int run_pc_head(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std
     }
     if (e != hipSuccess) return fail(ZFFT_ENOMEM, "decimator workspace allocation failed");
   }
-  int rc = run_pc(p, in, L, frames, n, walk, &cur, st, kPcStages);
+  int rc = run_pc(p, in, L, frames, n, walk, &cur, st, kPcStages, fc);
   if (rc) return rc;
   if (!xa_tail) {
     // zoom 2's tiles (XA's factorisation, the unit LO table) while a stage's input has >= 16384
@@ -1096,14 +1106,17 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
     return run_pc(p, in, L, frames, n, p->path >= 5 || (p->path == 0 && frames >= kPc4WalkMinFrames), out,
                   st, p->K);
   const bool walk = p->path >= 5 || (p->path == 0 && frames >= kPcWalkMinFrames);
-  // PC is the fastest schedule wherever it applies, from one frame per call (the
-  // reference's use: 0.083 against 0.37 ms for path 1) to full batches (1024 frames: 1.44
-  // against 2.03 ms for XA) -- tools/sweep_schedule.py, profiles/r04l
+  // FC in the walk's place: on request (6) and automatic from kFcMinFrames frames per call
+  const bool fc = fc_fits(p, L) && (p->path == 6 || (p->path == 0 && frames >= kFcMinFrames));
+  // PC (tiles below kFcMinFrames frames per call, FC from there) is the fastest schedule
+  // wherever it applies, from one frame per call (the reference's use: 0.053 against 0.37 ms
+  // for path 1) to full batches (4096 frames: FC 3.44 against the walk's 4.69 ms) --
+  // tools/sweep_schedule.py, profiles/r04l; tools/fc_ab.py, profiles/r06fc3
   if (pc8 && (p->path == 0 || p->path >= 4))
-    return run_pc(p, in, L, frames, n, walk, out, st, p->K, p->path == 6);
+    return run_pc(p, in, L, frames, n, walk || fc, out, st, p->K, fc);
   // zoom >= 16: the head, then XA or the blocked passes for the rest (by the tail's batch)
   if (p->path >= 4 || (p->path == 0 && head && xa_fits(p, L)))
-    return run_pc_head(p, in, L, frames, n, walk, out, st);
+    return run_pc_head(p, in, L, frames, n, walk || fc, out, st, fc);
   if (p->path == 3 || (p->path == 0 && auto_xa(frames, L) && xa_fits(p, L)))
     return run_xa(p, in, frames, n, out, st);
   if (use_fused(p, L, frames)) return run_fused(p, in, L, frames, n, out, st);
@@ -1596,6 +1609,8 @@ int zfft_decimate(zfft_plan *p, const void *iq, int64_t L, void *out_iq, int64_t
   if (rc) return rc;
   e = hipMemcpyAsync(p->in.p, iq, in_bytes, hipMemcpyHostToDevice, p->stream);
   if (e != hipSuccess) return hip_fail(e, "H2D copy");
+  p->n_marks = 0;  // timings of this call's launches (the first one was unnamed before)
+  mark(p, p->stream, "start");
   const float2 *x;
   if (p->K == 0) {  // zoomfft(x, 1) still mixes (S:2093-2094)
     e = p->dec.ensure((size_t)L * sizeof(float2));

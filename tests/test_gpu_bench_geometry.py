@@ -42,11 +42,11 @@ def test_bench_batch_rows_vs_oracle(oracle_lib, torch_dev, config, in_dtype):
         plan.process_device(xe.data_ptr(), L, F, rows.data_ptr(), st.cuda_stream)
         torch.cuda.synchronize()
         names = plan.launch_names()
-    assert names[0] in ("xa_stage_mix", "pc_fir", "pc_walk", "pc_walk4"), names  # the schedule the bench times
+    assert names[0] in ("xa_stage_mix", "pc_fir", "pc_walk", "pc_walk4", "fc_decim"), names  # the schedule the bench times
     if config == "cfg1":
         assert names[0] == "pc_walk4", names  # zoom 4 at F = 4096: the walk (round 6, r06k)
-    if config == "cfg5":
-        assert names[0] == "pc_walk", names  # F = 2048 frames of 2^20 samples: the walk (r06k)
+    if config in ("cfg2", "cfg3", "cfg5"):
+        assert names[0] == "fc_decim", names  # zoom 8 from 16 frames per call: FC (round 6, r06fc3)
     host = rows.cpu().numpy()
     assert np.isfinite(host).all()
     for f in PICK(F):

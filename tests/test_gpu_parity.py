@@ -483,9 +483,10 @@ def test_facade_matches_reference_rows():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("z,F,L,want", [(8, 1, 299008, "pc"), (8, 384, 299008, "pc"),
-                                        (8, 768, 1048576, "pc"), (8, 1024, 32768, "walk"),
-                                        (8, 1023, 32768, "pc"), (8, 4, 8192, "exact"),
+@pytest.mark.parametrize("z,F,L,want", [(8, 1, 299008, "pc"), (8, 15, 299008, "pc"),
+                                        (8, 16, 299008, "fc"), (8, 384, 299008, "fc"),
+                                        (8, 768, 1048576, "fc"), (8, 1024, 32768, "fc"),
+                                        (8, 1023, 32768, "fc"), (8, 4, 8192, "exact"),
                                         (4, 1, 262144, "pc"), (4, 256, 262144, "pc"),
                                         (4, 384, 262144, "pc"), (4, 64, 1048576, "pc"),
                                         (4, 511, 65536, "pc"), (4, 512, 65536, "walk4"),
@@ -493,7 +494,7 @@ def test_facade_matches_reference_rows():
                                         (2, 512, 65536, "xa"), (2, 511, 65536, "pc2"), (2, 8, 262144, "pc2"),
                                         (2, 600, 1048576, "pc2"), (2, 768, 1048576, "xa"),
                                         (2, 8, 8192, "exact"),
-                                        (16, 384, 262144, "pc"), (16, 512, 262144, "pc"),
+                                        (16, 384, 262144, "fc"), (16, 512, 262144, "fc"),
                                         (16, 8, 262144, "pc")])
 def test_auto_schedule_by_batch(z, F, L, want):
     """The automatic decimator schedule follows the measured crossovers (zfft_plan.cpp
@@ -522,6 +523,7 @@ def test_auto_schedule_by_batch(z, F, L, want):
         names = plan.launch_names()
     first = {"exact": ("exact_forward_mix",), "fused": ("exact_forward_mix",),
              "xa": ("xa_stage_mix",), "pc": ("pc_fir",), "pc2": ("pc_tail",), "walk": ("pc_walk",),
+             "fc": ("fc_decim",),
              "walk4": ("pc_walk4",)}[want]
     assert names[0] in first, names
     assert ("edge_windows" in names) == (want == "fused"), names
@@ -590,7 +592,7 @@ def test_xa_refuses_frames_beyond_32bit_offsets():
                                 torch.cuda.current_stream().cuda_stream)
 
 
-@pytest.mark.parametrize("z,F,L,first,waits", [(8, 1024, 32768, "pc_fir", 1), (4, 2100, 32768, "pc_walk4", 1),
+@pytest.mark.parametrize("z,F,L,first,waits", [(8, 1024, 32768, "fc_decim", 1), (4, 2100, 32768, "pc_walk4", 1),
                                                 (2, 2100, 32768, "xa_stage_mix", 1), (2, 500, 32768, "pc_tail", 1),
                                                 (4, 500, 32768, "pc_fir", 1)])
 def test_batched_host_call_times_every_batch_with_one_schedule(z, F, L, first, waits):
@@ -649,10 +651,10 @@ def test_lo_rows_refused_at_zoom_1():
         plan.set_lo_frames([], 1)
 
 
-@pytest.mark.parametrize("path,first", [(0, "pc_walk"), (4, "pc_fir"), (3, "xa_stage_mix")])
+@pytest.mark.parametrize("path,first", [(0, "fc_decim"), (5, "pc_walk"), (4, "pc_fir"), (3, "xa_stage_mix")])
 def test_lo_per_frame_bench_batch(oracle_lib, path, first):
     """Config 4 at the bench's geometry: 8 IFs x 512 frames of cfg2 in one F = 4096 batch on
-    the device (the automatic schedule -- the PC walk at this batch --, the PC tiles and XA),
+    the device (the automatic schedule -- FC at this batch --, the walk, the PC tiles and XA),
     two frames of every IF vs the oracle at that IF's f_LO."""
     import torch
     import bench

@@ -274,8 +274,8 @@ def test_pc_head_golden_rows(path):
 
 
 def test_pc_head_auto_batch_rows(oracle_lib):
-    """At a batch XA would take (384 frames), zoom 16 runs the PC head + one XA stage on its
-    own (the XA tail); rows of three frames against the oracle."""
+    """At a batch XA would take (384 frames), zoom 16 runs the head (FC from 16 frames per call)
+    + one XA stage on its own (the XA tail); rows of three frames against the oracle."""
     from pypanadapter_amd import ZoomFFT
     F, L, N = 384, 65536 + 3, 2048
     x = np.zeros((F, L), np.complex64)
@@ -285,7 +285,7 @@ def test_pc_head_auto_batch_rows(oracle_lib):
         plan.set_timing(True)
         rows = plan.rows(x)
         names = plan.launch_names()
-    assert names[0] == "pc_fir" and "xa_stage" in names and "pc_edge" in names, names
+    assert names[0] == "fc_decim" and "xa_stage" in names and "pc_edge" in names, names
     for f in (0, 191, F - 1):
         assert_row_close(rows[f], oracle_lib.psd_row(x[f], 2.4e6, N, 16, 128), f"frame {f}")
 
@@ -310,7 +310,7 @@ def test_pc2_decimate_vs_oracle(oracle_lib, flip):
             plan.set_timing(True)
             d = plan.decimate(x)
             names = plan.launch_names()
-        assert names[-1] == "pc_edge", names  # (decimate marks no start: its first launch is unnamed)
+        assert names[-1] == "pc_edge", names
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 2, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
         check_rel(d, ref, PC_TOL, "pc2/decimate", (L, flip))

@@ -13,7 +13,7 @@ STEPS="${*:-tests smoke bench prof}"
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-FAST="--no-cpu --no-e2e --no-check"
+FAST="--no-cpu --no-e2e --no-check ${BENCH_EXTRA:-}"  # BENCH_EXTRA: e.g. --path 6 for A/B profiles
 
 run() {  # name seconds cmd...
   local name=$1 to=$2
