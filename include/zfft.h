@@ -211,20 +211,20 @@ int zfft_plan_timings(zfft_plan *plan, float *ms_out, int32_t max, int32_t *coun
 const char *zfft_plan_timing_names(zfft_plan *plan);
 
 /* Decimator schedule: 0 = automatic -- for zoom 8 and frames of >= 16384 samples 4 below
- * 1024 frames per call and 5 from there (zoom >= 16: the same for the first three stages;
- * zoom 4: 4 below 512 frames per call and 5 from there; zoom 2: 4 below 512); otherwise 3 for
+ * 16 frames per call and 6 from there (zoom >= 16: the same for the first three stages;
+ * zoom 4: 4 below 32 frames per call and 6 from there; zoom 2: 4 below 512); otherwise 3 for
  * batches of >= 768 frames, or >= 384 frames of <= 2^19
  * samples, else 2 for batches of >= 2^27 samples whose frames are long enough for the edge
  * windows, else 1 -- e.g. one frame per call, the reference's use.  Each batch of a
  * zfft_process call is judged by its own frame count (host calls are split into batches of
- * about 1 GiB of input -- 418 cfg2 frames -- so from host memory path 5 is reached only by
- * forcing it; zfft_process_device judges the whole call); crossovers measured by
- * tools/sweep_schedule.py (profiles/r04v/sweep_schedule.json).  Default tolerance: the
- * automatic PC choices (zoom 8 at every batch, zoom 4 below 1024 frames per call, zoom 2
- * below 512) give the float64 reference's decimated IQ within 6.5e-6 of its peak, the head
- * of zoom >= 16 (PC's x8 + zoom 2's tiles or the blocked passes) within 7.5e-6 -- the
- * measured worst of the GPU tests + ~20 % (5.35e-6 and 6.02e-6; the walk on the zf_n512_z8
- * fixture 6.07e-6; tests/test_gpu_pc.py PC_TOL / HEAD_TOL); path 1: 2e-6.
+ * about 1 GiB of input -- 418 cfg2 frames); crossovers measured by tools/sweep_schedule.py,
+ * tools/sweep_walk.py and tools/fc_ab.py (profiles/r04v, r06k, r06fc).  Default tolerance:
+ * path 6 gives the float64 reference's decimated IQ within 6.5e-7 of its peak (measured
+ * worst 6.0e-7, tests/test_gpu_fc.py FC_TOL); the PC choices (zoom 8 below 16 frames per call,
+ * zoom 4 below 32, zoom 2 below 512) within 6.5e-6, the head of zoom >= 16 (x8 + zoom 2's tiles or the
+ * blocked passes) within 7.5e-6 -- the measured worst of the GPU tests + ~20 % (5.35e-6 and
+ * 6.02e-6; the walk on the zf_n512_z8 fixture 6.07e-6; tests/test_gpu_pc.py PC_TOL / HEAD_TOL);
+ * path 1: 2e-6.
  * 1 = blocked warm-up passes in the reference order (frames split over many waves),
  * 2 = blocked, fused commuted-order interior + exact edge windows, 3 = XA tiles (one wave per
  * frame and stage: all-pole cascade + 25-tap FIR + half-rate all-pole, lane states scanned;
@@ -234,18 +234,25 @@ const char *zfft_plan_timing_names(zfft_plan *plan);
  * rank-~10 frame-end maps; frames >= 16384 samples, <= 65535 frames per launch; zoom 4, 2
  * and the head of zoom >= 16 as below), 5 = the
  * same arithmetic as one launch with one workgroup per frame (the rate-1/4 intermediate
- * stays on chip; automatic from 1024 frames per call); at zoom 4, path 5 is the two-stage
- * form of the walk (FIR, own-rate sections at rate 1/2, 41-tap FIR, 6 output-rate sections;
- * automatic from 512 frames per call) and path 4 its tiles (automatic below that); at zoom 2,
+ * stays on chip); at zoom 4, path 5 is the two-stage
+ * form of the walk (FIR, own-rate sections at rate 1/2, 41-tap FIR, 6 output-rate sections)
+ * and path 4 its tiles (automatic below 32 frames per call); at zoom 2,
  * paths 4 / 5 run one-stage tiles in XA's factorisation (the
  * 4 sections forward at the input rate, a 25-tap FIR, their squares backward at half rate;
- * automatic below 512 frames per call); at zoom >= 16, paths 4 / 5 run PC (tiles / walk) for the
+ * automatic below 512 frames per call); at zoom >= 16, paths 4 / 5 / 6 run PC / FC for the
  * first three stages and XA for the rest on its 1/8-rate output -- the automatic choice
- * wherever XA would take the batch (zoom 16 on cfg2's frames: 5.23 against XA's 6.35 ms per
- * 4096 frames).  Path 3
+ * wherever XA would take the batch (zoom 16 on cfg2's frames: 3.64 ms per 4096 frames with FC,
+ * 5.01 with the walk, 6.35 with XA alone); 6 = FC, fast convolution (zoom 8, zoom 4 and the head
+ * of zoom >= 16; elsewhere as 5): the model's impulse response truncated at |k| <= 768 (zoom 8)
+ * / 512 (zoom 4) input samples (tail <= 1e-6 of its absolute sum) applied by overlap-save in
+ * 8192-sample windows -- the residues' DFTs, the decimation folded into the spectrum with the
+ * filter and the LO's modulation, one inverse DFT per window, one launch with one workgroup
+ * per frame (or per run of windows below 1024 frames per call), the frame-end maps as for 5;
+ * frames of >= 8192 samples below 2^31 bytes (cfg2's 4096 frames: 2.66 ms against the walk's
+ * 4.18; cfg1's: 2.82 against the zoom-4 walk's 4.22).  Path 3
  * needs every stage array below 2^31 bytes per frame; a forced path outside its domain
  * returns ZFFT_EUNSUPPORTED.  All produce the reference's rows within the fp32 parity gate
- * (zfft_plan.cpp auto_xa, use_fused, pc_fits). */
+ * (zfft_plan.cpp auto_xa, use_fused, pc_fits, fc_fits). */
 int zfft_plan_path(zfft_plan *plan, int32_t path);
 
 /* Batched multi-IF (BASELINE config 4): one LO frequency per group of frames in a single

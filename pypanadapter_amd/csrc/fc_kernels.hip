@@ -49,19 +49,18 @@ namespace fc {
 typedef v2f __attribute__((address_space(3))) *LP;
 typedef v4f __attribute__((address_space(3))) *LP4;
 
-constexpr int kN = kFcN, kM = kFcN / 8;  // window, per-residue transform
-constexpr int kS = kFcStep;              // 512-sample chunks a block advances
-constexpr int kK = kFcK;                 // half length of the truncated response
-constexpr int kP = kFcP;                 // outputs per block
-constexpr int kKeep = 16 - kS;           // a thread's pairs carried into the next window
-constexpr int kJ0 = kK / 8;              // first valid inverse output
-static_assert(kK == (kN - 512 * kS) / 2 && kP == 64 * kS && kK % 8 == 0 && kKeep >= 1, "FC block geometry");
-static_assert(kJ0 + kP <= 1024 && kJ0 < 256 && kJ0 + kP > 768, "outputs: three or four per thread");
+// Block geometry per zoom (zfft_internal.h): Z residues of an M = 8192 / Z point DFT; a block
+// advances 512 S samples and makes P = 512 S / Z outputs; K = (8192 - 512 S) / 2.
+template <int Z> struct Geo;
+template <> struct Geo<8> { static constexpr int S = kFcStep, K = kFcK, P = kFcP; };
+template <> struct Geo<4> { static constexpr int S = kFc4Step, K = kFc4K, P = kFc4P; };
+constexpr int kN = kFcN;
 // LDS: the window as [pos][residue] with 2 pad slots per 32 (conflict-free b128 reads in all
-// three forward passes, tools/fc_model.py layout check); the inverse 1024 points, 1 pad per 16
+// three forward passes, tools/fc_model.py layout check); the inverse M points, 1 pad per 16 --
+// its own array at zoom 8 (1024 points), inside the window's at zoom 4 (2048: two arrays would
+// not fit two workgroups per CU)
 constexpr int kBigSlots = kN + 2 * (kN / 32);
-constexpr int kSmallSlots = kM + kM / 16;
-__device__ __forceinline__ int pb(int i) { return i + 2 * (i >> 5); }
+constexpr int kSmallSlots8 = 1024 + 1024 / 16;
 __device__ __forceinline__ int ps(int i) { return i + (i >> 4); }
 
 // acc + a b (complex) in two VOP3P instructions (cmul2 with the accumulator as the addend)
@@ -73,19 +72,37 @@ __device__ __forceinline__ v2f cmac2(v2f acc, v2f a, v2f b) {
   return r;
 }
 __device__ __forceinline__ v2f conj(v2f a) { return v2f{a.x, -a.y}; }
-// sum_a v_a W_4^(-ab): the forward radix 4 with outputs 1 and 3 exchanged
-__device__ __forceinline__ void idft4(v2f *v) {
-  dft<4>(v);
-  const v2f s = v[1];
-  v[1] = v[3];
-  v[3] = s;
+// sum_a v_a W_R^(-ab): the forward radix R with outputs b and R - b exchanged
+template <int R>
+__device__ __forceinline__ void idft(v2f *v) {
+  dft<R>(v);
+#pragma unroll
+  for (int b = 1; b < R / 2; ++b) {
+    const v2f s = v[b];
+    v[b] = v[R - b];
+    v[R - b] = s;
+  }
 }
-// v[b] *= w^b, b = 1..3
-__device__ __forceinline__ void pow_tw3(v2f *v, v2f w) {
+// v[b] *= w^b, b = 1 .. R-1 (R = 4, 8)
+template <int R>
+__device__ __forceinline__ void pow_tw(v2f *v, v2f w);
+template <>
+__device__ __forceinline__ void pow_tw<4>(v2f *v, v2f w) {
   const v2f w2 = cmul2(w, w);
   v[1] = cmul2(v[1], w);
   v[2] = cmul2(v[2], w2);
   v[3] = cmul2(v[3], cmul2(w2, w));
+}
+template <>
+__device__ __forceinline__ void pow_tw<8>(v2f *v, v2f w) {  // each power from at most 3 products
+  const v2f w2 = cmul2(w, w), w4 = cmul2(w2, w2), w3 = cmul2(w2, w);
+  v[1] = cmul2(v[1], w);
+  v[2] = cmul2(v[2], w2);
+  v[3] = cmul2(v[3], w3);
+  v[4] = cmul2(v[4], w4);
+  v[5] = cmul2(v[5], cmul2(w4, w));
+  v[6] = cmul2(v[6], cmul2(w4, w2));
+  v[7] = cmul2(v[7], cmul2(w4, w3));
 }
 
 // Loads through buffer resources: one lane offset VGPR and constant SGPR offsets per load (64-bit
@@ -139,66 +156,82 @@ __device__ __forceinline__ typename RawP<DT>::T load_pair_b(__amdgpu_buffer_rsrc
   else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, aux));
 }
 
-// One workgroup walks blocks [bpc * blockIdx.x, +bpc) of frame blockIdx.y.  tab: W_1024^k
-// (k < 1024), then per LO row (row_stride apart) C as v4f pairs [4 k3 + r / 2][t] (r, r + 1) for
-// thread t of pass C.  Needs frames of >= kFcN samples and < 2^31 bytes (launch_fc_decim).
-template <int DT, int FLIP>
+// One workgroup walks blocks [bpc * blockIdx.x, +bpc) of frame blockIdx.y.  tab: W_M^k (k < M),
+// then per LO row (row_stride apart) C as v4f pairs [(Z / 2) k3 + r / 2][t] (r, r + 1) for thread t
+// of pass C.  Needs frames of >= kFcN samples and < 2^31 bytes (launch_fc_decim).
+template <int Z, int DT, int FLIP>
 __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *lo, const v2f *tab,
-                                                         int64_t row_stride, v2f *out, int64_t n3,
+                                                         int64_t row_stride, v2f *out, int64_t nd,
                                                          int bpc) {
+  constexpr int M = kN / Z;             // per-residue transform: 1024 (zoom 8), 2048 (zoom 4)
+  constexpr int R1 = M / 256;           // radix of the last forward / first inverse stage
+  constexpr int S = Geo<Z>::S, K = Geo<Z>::K, P = Geo<Z>::P;
+  constexpr int KEEP = 16 - S;          // a thread's pairs carried into the next window
+  constexpr int J0 = K / Z;             // first valid inverse output
+  constexpr int NB = M / 1024;          // inverse butterflies per thread in stages 2..5
+  constexpr bool ALIAS = Z == 4;        // the inverse array inside the window's
+  static_assert(K == (kN - 512 * S) / 2 && P * Z == 512 * S && K % Z == 0 && KEEP >= 1, "FC block geometry");
+  static_assert(J0 + P <= M && J0 < 256 * NB, "FC outputs");
   __shared__ v4f big4[kBigSlots / 2];
-  __shared__ v2f small_[kSmallSlots];
+  __shared__ v2f small_[ALIAS ? 2 : kSmallSlots8];
   const LP bl = (LP)big4;
-  const LP sl = (LP)small_;
+  const LP sl = ALIAS ? bl : (LP)small_;
   const int t = threadIdx.x;
   const int64_t f = blockIdx.y, L = in.len;
-  const int nb = (int)((n3 + kP - 1) / kP);
+  const int nb = (int)((nd + P - 1) / P);
   const int b0 = (int)blockIdx.x * bpc, b1 = min(nb, b0 + bpc);
   if (b0 >= b1) return;
   const v2f *lor = lo_row(lo, in, f);
   const int row = in.lo_n <= 1 ? 0 : (int)((((int64_t)in.lo_first + f) / in.lo_per) % in.lo_n);
   const v2f *tw = tab;
   const __amdgpu_buffer_rsrc_t crs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)(tab + kM + row * row_stride), (short)0, kFcRow * 8, kBufFlags);
+      __builtin_amdgcn_make_buffer_rsrc((void *)(tab + M + row * row_stride), (short)0, kFcRow * 8, kBufFlags);
   const __amdgpu_buffer_rsrc_t xrs = frame_rsrc<DT>(in, f);
-  // pass A: j0 = t >> 2 (residues 2 (t & 3), +1); pass B: k1 = t >> 4, j1 = (t >> 2) & 3
+  // pass A: residues of thread t's pairs 2t + 512 i are (2t mod Z, +1), at m = j0 + (M / 16) i;
+  // pass B: k1 = t >> 4, j1 = the digit below i2 of the (M / 16)-point remainder
+  const int j0 = t >> (Z == 8 ? 2 : 1), j1 = Z == 8 ? (t >> 2) & 3 : (t >> 1) & 7;
   v2f bA[4], bB[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    bA[s] = tw[((t >> 2) << s) & (kM - 1)];
-    bB[s] = tw[((16 * ((t >> 2) & 3)) << s) & (kM - 1)];
+    bA[s] = tw[(j0 << s) & (M - 1)];
+    bB[s] = tw[((16 * j1) << s) & (M - 1)];
   }
   // pass C: k1 = t >> 4, k2 = t & 15 -> kp = k1 + 16 k2
   const int kp = (t >> 4) + 16 * (t & 15);
-  // inverse twiddle bases, conjugated: stage 1 W^kp, 2 W^(4 (t & 63)), 3 W^(16 (t & 15)),
-  // 4 W^(64 (t & 3)) (the digits below each stage's)
-  const v2f ib0 = conj(tw[kp]), ib1 = conj(tw[4 * (t & 63)]), ib2 = conj(tw[16 * (t & 15)]),
-            ib3 = conj(tw[64 * (t & 3)]);
-  // outputs: j = t + 256 b4, valid for j in [kJ0, kJ0 + kP) (three or four per thread), at
-  // output jm = j - kJ0 of the block; their lo[8 jm] (0 where invalid or past the frame)
-  v2f lj[4];
+  // inverse twiddle bases, conjugated: stage 1 W_M^kp, 2 W_256^(t & 63), 3 W_64^(t & 15),
+  // 4 W_16^(t & 3) (the digits below each stage's)
+  const v2f ib0 = conj(tw[kp]), ib1 = conj(tw[(M / 256) * (t & 63)]), ib2 = conj(tw[(M / 64) * (t & 15)]),
+            ib3 = conj(tw[(M / 16) * (t & 3)]);
+  // outputs: butterfly u = t + 256 h of stage 5 gives j = u + (M / 4) b4, valid for j in
+  // [J0, J0 + P), at output jm = j - J0 of the block; their lo[Z jm] (0 where invalid / past
+  // the frame)
+  v2f lj[NB][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int jm = t + 256 * q - kJ0;
-    lj[q] = jm >= 0 && jm < kP && jm < n3 ? lor[8 * jm] : splat(0.f);
-  }
-  // LDS bases (v2f slots; the pads of pb / ps folded into the constant strides)
+  for (int h = 0; h < NB; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int jm = t + 256 * h + (M / 4) * q - J0;
+      lj[h][q] = jm >= 0 && jm < P && jm < nd ? lor[Z * jm] : splat(0.f);
+    }
+  // LDS bases (v2f slots; the pads folded into the constant strides)
   const int aA = 2 * t + 2 * (t >> 4);                 // pb(512 k + 2t) = aA + 544 k
   const int aB = 2 * (t & 15) + 544 * (t >> 4);        // pb(base + 32 i) = aB + 34 i
-  const int aC = 544 * (t >> 4) + 34 * (t & 15);       // pb(.. + 8 j + 2 rp) = aC + 8 j + 2 rp
-  const int a1 = kp + (kp >> 4);                       // ps(kp + 256 q) = a1 + 272 q
-  const int i2 = (t & 63) + 256 * (t >> 6), a2 = i2 + (i2 >> 4);                          // + 68 a
-  const int i3 = (t & 15) + 64 * ((t >> 4) & 3) + 256 * (t >> 6), a3 = i3 + (i3 >> 4);   // + 17 a
-  const int i4 = (t & 3) + 16 * ((t >> 2) & 3) + 64 * ((t >> 4) & 3) + 256 * (t >> 6);
-  const int a4 = i4 + (i4 >> 4);                                                         // + 4 a
-  const int i5 = 4 * (t >> 6) + 16 * ((t >> 4) & 3) + 64 * ((t >> 2) & 3) + 256 * (t & 3);
-  const int a5 = i5 + (i5 >> 4);                                                          // + a
+  const int aC = 544 * (t >> 4) + 34 * (t & 15);       // pair p of pass C: aC + 2 p
+  const int a1 = ps(kp);                               // ps(kp + 256 q) = a1 + 272 q
+  // stages 2..4 (butterfly t + 256 h at +1088 h), stage 5
+  const int a2 = ps((t & 63) + 256 * (t >> 6));                                      // + 68 a
+  const int a3 = ps((t & 15) + 64 * ((t >> 4) & 3) + 256 * (t >> 6));               // + 17 a
+  const int a4 = ps((t & 3) + 16 * ((t >> 2) & 3) + 64 * ((t >> 4) & 3) + 256 * (t >> 6));  // + 4 a
+  auto a5 = [&](int h) {  // u = b0 + R1 (b1 + 4 b2 + 16 b3) reads (a0 + 4 b3 + 16 b2 + 64 b1 + 256 b0)
+    const int u = t + 256 * h, r = u / R1;
+    return ps(4 * ((r >> 4) & 3) + 16 * ((r >> 2) & 3) + 64 * (r & 3) + 256 * (u % R1));
+  };
 
-  auto wstart = [&](int b) -> int64_t { return (int64_t)(512 * kS) * b - kK; };
+  auto wstart = [&](int b) -> int64_t { return (int64_t)(512 * S) * b - K; };
   auto inside = [&](int b) { const int64_t s = wstart(b); return s >= 0 && s + kN <= L; };
-  typename RawP<DT>::T pf[kS];  // the next window's pairs kKeep .. 15
-  v2f ka[kKeep], kb[kKeep];     // this window's pairs kS .. 15 = the next window's 0 .. kKeep-1
-  bool carried = false;         // ka, kb and pf hold this block's window
+  typename RawP<DT>::T pf[S];  // the next window's pairs KEEP .. 15
+  v2f ka[KEEP], kb[KEEP];      // this window's pairs S .. 15 = the next window's 0 .. KEEP-1
+  bool carried = false;        // ka, kb and pf hold this block's window
   // the next window's new pairs, issued on every block from a window start clamped into the
   // frame (values unused when the next window is not inside it): one unconditional call site,
   // so the wait before their use counts only what was issued after them
@@ -208,15 +241,15 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
     sn = sn < 0 ? 0 : (sn > L - kN ? L - kN : sn);
     const uint32_t vo = pair_vo<DT, FLIP>(L, sn, t);
 #pragma unroll
-    for (int i = 0; i < kS; ++i)
-      if (!(FC_KO & 1)) pf[i] = load_pair_b<DT, FLIP>(xrs, vo, kKeep + i);
+    for (int i = 0; i < S; ++i)
+      if (!(FC_KO & 1)) pf[i] = load_pair_b<DT, FLIP>(xrs, vo, KEEP + i);
   };
   for (int b = b0; b < b1; ++b) {
     v2f xa[16], xb[16];
-    // this block's lo[8 m0], requested before the prefetch: its wait at the outputs then
+    // this block's lo[Z m0], requested before the prefetch: its wait at the outputs then
     // leaves the prefetch in flight (the vector-memory counter completes in order)
-    const int64_t m0 = (int64_t)kP * b;
-    const v2f lob = lor[8 * m0];
+    const int64_t m0 = (int64_t)P * b;
+    const v2f lob = lor[Z * m0];
     {
       const int64_t s = wstart(b);
       if (FC_KO & 1) {
@@ -227,12 +260,12 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
         }
       } else if (carried) {
 #pragma unroll
-        for (int i = 0; i < kKeep; ++i) {
+        for (int i = 0; i < KEEP; ++i) {
           xa[i] = ka[i];
           xb[i] = kb[i];
         }
 #pragma unroll
-        for (int i = 0; i < kS; ++i) cvt_pair<DT, FLIP>(pf[i], xa[kKeep + i], xb[kKeep + i]);
+        for (int i = 0; i < S; ++i) cvt_pair<DT, FLIP>(pf[i], xa[KEEP + i], xb[KEEP + i]);
       } else {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -242,20 +275,21 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
         }
       }
 #pragma unroll
-      for (int i = 0; i < kKeep; ++i) {
-        ka[i] = xa[kS + i];
-        kb[i] = xb[kS + i];
+      for (int i = 0; i < KEEP; ++i) {
+        ka[i] = xa[S + i];
+        kb[i] = xb[S + i];
       }
       issue_pf(b);
     }
-    // pass A: DFT16 over i (m = j0 + 64 i) -> k1, twiddle W_1024^(j0 k1), to LDS at (64 k1 + j0, r)
+    // pass A: DFT16 over i -> k1, twiddle W_M^(j0 k1), to LDS at ((M / 16) k1 + j0, r)
     dft<16>(xa);
     dft<16>(xb);
     apply_powers2(xa, xb, bA);
 #pragma unroll
     for (int k = 0; k < 16; ++k) *(LP4)(bl + aA + 544 * k) = cat(xa[k], xb[k]);
     __syncthreads();
-    // pass B: (64 k1 + j1 + 4 i2) -> DFT16 over i2 -> k2, twiddle W_64^(j1 k2), in place
+    // pass B: ((M / 16) k1 + j1 + (M / 256) i2) -> DFT16 over i2 -> k2, twiddle
+    // W_(M / 16)^(j1 k2), in place
     {
       v2f ya[16], yb[16];
 #pragma unroll
@@ -271,49 +305,56 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
       for (int k = 0; k < 16; ++k) *(LP4)(bl + aB + 34 * k) = cat(ya[k], yb[k]);
     }
     __syncthreads();
-    // pass C: (64 k1 + 4 k2 + j1, r) for all j1, r -> DFT4 over j1 -> k3; Yf = sum_r A_r C;
-    // inverse stage 1 (radix 4 over k3 -> b0, twiddle W_1024^(-b0 kp)) to (kp + 256 b0)
+    // pass C: ((M / 16) k1 + R1 k2 + j1, r) for all j1 < R1, r < Z -> DFT_R1 over j1 -> k3;
+    // Yf = sum_r A_r C; inverse stage 1 (radix R1 over k3 -> b0, twiddle W_M^(-b0 kp)) to
+    // (kp + 256 b0)
     {
       v4f cr[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         cr[i] = (FC_KO & 2) ? v4f{1.f, 0.5f, 0.25f, 1.f}
                             : __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(crs, (uint32_t)(16 * t), 4096 * i, 0));
-      // one residue pair at a time: its four j1 values, DFT4 each, accumulated into Yf (the
-      // whole window's 32 values and C's 32 at once spilled)
-      v2f yf[4] = {splat(0.f), splat(0.f), splat(0.f), splat(0.f)};
+      // one residue pair at a time: its R1 values, DFT each, accumulated into Yf (the whole
+      // window's 32 values and C's 32 at once spilled)
+      v2f yf[R1];
 #pragma unroll
-      for (int rp = 0; rp < 4; ++rp) {
-        v2f ea[4], eb[4];
+      for (int k = 0; k < R1; ++k) yf[k] = splat(0.f);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const v4f w = *(LP4)(bl + aC + 8 * j + 2 * rp);
+      for (int rp = 0; rp < Z / 2; ++rp) {
+        v2f ea[R1], eb[R1];
+#pragma unroll
+        for (int j = 0; j < R1; ++j) {
+          const v4f w = *(LP4)(bl + aC + 2 * (Z / 2 * j + rp));
           ea[j] = lo2(w);
           eb[j] = hi2(w);
         }
-        dft<4>(ea);
-        dft<4>(eb);
+        dft<R1>(ea);
+        dft<R1>(eb);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const v4f c = cr[4 * k + rp];
+        for (int k = 0; k < R1; ++k) {
+          const v4f c = cr[Z / 2 * k + rp];
           yf[k] = cmac2(cmac2(yf[k], ea[k], lo2(c)), eb[k], hi2(c));
         }
       }
-      idft4(yf);
-      pow_tw3(yf, ib0);
+      idft<R1>(yf);
+      pow_tw<R1>(yf, ib0);
+      if (ALIAS) __syncthreads();  // every pass-C read done before the inverse array overwrites
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sl[a1 + 272 * q] = yf[q];
+      for (int q = 0; q < R1; ++q) sl[a1 + 272 * q] = yf[q];
     }
     __syncthreads();
     // inverse stages 2..4: radix 4 over the digit at stride S, twiddle W_(4S)^(-b k_low)
     auto istage = [&](int a0, int st, v2f w) {
-      v2f v[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) v[a] = sl[a0 + st * a];
-      idft4(v);
-      pow_tw3(v, w);
+      for (int h = 0; h < NB; ++h) {
+        v2f v[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) sl[a0 + st * a] = v[a];
+        for (int a = 0; a < 4; ++a) v[a] = sl[a0 + 1088 * h + st * a];
+        idft<4>(v);
+        pow_tw<4>(v, w);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) sl[a0 + 1088 * h + st * a] = v[a];
+      }
     };
     istage(a2, 68, ib1);
     __syncthreads();
@@ -321,29 +362,37 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
     __syncthreads();
     istage(a4, 4, ib3);
     __syncthreads();
-    // stage 5: t = b0 + 4 b1 + 16 b2 + 64 b3 reads (a0 + 4 b3 + 16 b2 + 64 b1 + 256 b0) -> b4
+    // stage 5: radix 4 over a0 -> b4; outputs j = u + (M / 4) b4
     {
-      v2f v[4];
+      v2f *o = out + f * nd + m0;
 #pragma unroll
-      for (int a = 0; a < 4; ++a) v[a] = sl[a5 + a];
-      idft4(v);
-      v2f *o = out + f * n3 + m0;
+      for (int h = 0; h < NB; ++h) {
+        const int i5 = a5(h);
+        v2f v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int jm = t + 256 * q - kJ0;
-        if (jm >= 0 && jm < kP && m0 + jm < n3 && !(FC_KO & 4))
-          __builtin_nontemporal_store(cmul2(v[q], cmul2(lob, lj[q])), o + jm);
+        for (int a = 0; a < 4; ++a) v[a] = sl[i5 + a];
+        idft<4>(v);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int jm = t + 256 * h + (M / 4) * q - J0;
+          if (jm >= 0 && jm < P && m0 + jm < nd && !(FC_KO & 4))
+            __builtin_nontemporal_store(cmul2(v[q], cmul2(lob, lj[h][q])), o + jm);
+        }
       }
     }
+    if (ALIAS) __syncthreads();  // stage-5 reads done before the next window's pass-A stores
   }
 }
 
 }  // namespace fc
 
 hipError_t launch_fc_decim(const InDesc &in, const float2 *lo, const float2 *tab, int64_t row_stride,
-                           float2 *out, int64_t n3, int frames, hipStream_t st) {
-  if (in.len < kFcN || in.len * (int64_t)in_elem_bytes(in.dtype) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-  const int nb = (int)((n3 + kFcP - 1) / kFcP);
+                           float2 *out, int64_t nd, int frames, int zoom, hipStream_t st) {
+  if (in.len < kFcN || in.len * (int64_t)in_elem_bytes(in.dtype) >= ((int64_t)1 << 31) ||
+      (zoom != 8 && zoom != 4))
+    return hipErrorInvalidValue;
+  const int P = zoom == 8 ? kFcP : kFc4P;
+  const int nb = (int)((nd + P - 1) / P);
   // about two rounds of the chip's 512 resident workgroups: whole frames from 1024 frames per
   // call, below that each frame split into runs of blocks (a run's first window loads in full)
   const int chunks = std::max(1, std::min(nb, (1024 + frames - 1) / frames));
@@ -351,19 +400,23 @@ hipError_t launch_fc_decim(const InDesc &in, const float2 *lo, const float2 *tab
   const dim3 grid((unsigned)((nb + bpc - 1) / bpc), (unsigned)frames);
   const v2f *l = (const v2f *)lo, *tb = (const v2f *)tab;
   v2f *o = (v2f *)out;
-#define FC_GO(DT, FL) \
-  hipLaunchKernelGGL((fc::fc_decim_kernel<DT, FL>), grid, dim3(256), 0, st, in, l, tb, row_stride, o, n3, bpc)
-  if (in.flip) {
-    if (in.dtype == kInC64) FC_GO(kInC64, 1);
-    else if (in.dtype == kInC32H) FC_GO(kInC32H, 1);
-    else if (in.dtype == kInCU8) FC_GO(kInCU8, 1);
-    else FC_GO(kInF32R, 1);
+#define FC_GO(Z, DT, FL) \
+  hipLaunchKernelGGL((fc::fc_decim_kernel<Z, DT, FL>), grid, dim3(256), 0, st, in, l, tb, row_stride, o, nd, bpc)
+#define FC_DT(Z, FL)                           \
+  do {                                         \
+    if (in.dtype == kInC64) FC_GO(Z, kInC64, FL);        \
+    else if (in.dtype == kInC32H) FC_GO(Z, kInC32H, FL); \
+    else if (in.dtype == kInCU8) FC_GO(Z, kInCU8, FL);   \
+    else FC_GO(Z, kInF32R, FL);                          \
+  } while (0)
+  if (zoom == 8) {
+    if (in.flip) FC_DT(8, 1);
+    else FC_DT(8, 0);
   } else {
-    if (in.dtype == kInC64) FC_GO(kInC64, 0);
-    else if (in.dtype == kInC32H) FC_GO(kInC32H, 0);
-    else if (in.dtype == kInCU8) FC_GO(kInCU8, 0);
-    else FC_GO(kInF32R, 0);
+    if (in.flip) FC_DT(4, 1);
+    else FC_DT(4, 0);
   }
+#undef FC_DT
 #undef FC_GO
   return hipGetLastError();
 }

@@ -389,25 +389,27 @@ bool pc_edge_map(int side, int lmod8, PcEdge &out) { return pc_edge_map_k(3, sid
 
 // ---- FC tables (fc_kernels.hip; tools/fc_model.py c_table) ----
 
-void fc_build_twiddles(float2 *tw) {
-  for (int k = 0; k < kFcN / 8; ++k) {
-    const double a = -2.0 * M_PI * k / (kFcN / 8);
+void fc_build_twiddles(int M, float2 *tw) {
+  for (int k = 0; k < M; ++k) {
+    const double a = -2.0 * M_PI * k / M;
     tw[k] = make_float2((float)std::cos(a), (float)std::sin(a));
   }
 }
 
-// g'[k] = g[k] e^(2 pi i lo_ratio k), |k| <= kFcK (g = the zoom-8 model's input-rate response,
-// model_hz(3)), placed circularly in kFcN; G = its DFT; C[k][r] = W_N^(rk) sum_q G[k + M q] W_8^(rq)
-// / (N sqrt 2) for k < M = N / 8 (the 1 / sqrt 2: the outputs take lo[8m] as the composite
-// lo[a] lo[b] = sqrt 2 lo[a + b]).  Stored for pass C's thread t (k' = (t >> 4) + 16 (t & 15)):
-// row as v4f pairs: float2 index ((4 k3 + r / 2) 256 + t) 2 + r % 2 holds C[k' + 256 k3][r].
-bool fc_build_row(double lo_ratio, float2 *row) {
-  constexpr int N = kFcN, M = kFcN / 8;
-  const std::vector<double> &h = model_hz(kPcStages);
-  if ((int)h.size() < 2 * kFcK + 1) return false;
+// Zoom Z (8 or 4): g'[k] = g[k] e^(2 pi i lo_ratio k), |k| <= K (g = the zoom-Z model's input-rate
+// response, model_hz(log2 Z); K = kFcK or kFc4K), placed circularly in N = kFcN; G = its DFT;
+// C[k][r] = W_N^(rk) sum_(q < Z) G[k + M q] W_Z^(rq) / (N sqrt 2) for k < M = N / Z (the 1 / sqrt 2:
+// the outputs take lo[Z m] as the composite lo[a] lo[b] = sqrt 2 lo[a + b]).  Stored for pass C's
+// thread t (k' = (t >> 4) + 16 (t & 15), k = k' + 256 k3) as v4f pairs: float2 index
+// (((Z / 2) k3 + r / 2) 256 + t) 2 + r % 2 holds C[k][r].
+bool fc_build_row(int zoom, double lo_ratio, float2 *row) {
+  if (zoom != 8 && zoom != 4) return false;
+  const int N = kFcN, M = kFcN / zoom, K = zoom == 8 ? kFcK : kFc4K, R1 = M / 256;
+  const std::vector<double> &h = model_hz(zoom == 8 ? 3 : 2);
+  if ((int)h.size() < 2 * K + 1) return false;
   const int hc = ((int)h.size() - 1) / 2;
   std::vector<std::complex<double>> g(N, 0.0);
-  for (int k = -kFcK; k <= kFcK; ++k) {
+  for (int k = -K; k <= K; ++k) {
     const double turns = std::fmod(lo_ratio * (double)k, 1.0);
     g[(k + N) % N] = h[hc + k] * std::polar(1.0, 2.0 * M_PI * turns);
   }
@@ -415,13 +417,13 @@ bool fc_build_row(double lo_ratio, float2 *row) {
   const double s = 1.0 / ((double)N * std::sqrt(2.0));
   for (int t = 0; t < 256; ++t) {
     const int kp = (t >> 4) + 16 * (t & 15);
-    for (int k3 = 0; k3 < 4; ++k3) {
+    for (int k3 = 0; k3 < R1; ++k3) {
       const int k = kp + 256 * k3;
-      for (int r = 0; r < 8; ++r) {
+      for (int r = 0; r < zoom; ++r) {
         std::complex<double> c = 0.0;
-        for (int q = 0; q < 8; ++q) c += g[k + M * q] * std::polar(1.0, -2.0 * M_PI * ((r * q) % 8) / 8.0);
+        for (int q = 0; q < zoom; ++q) c += g[k + M * q] * std::polar(1.0, -2.0 * M_PI * ((r * q) % zoom) / zoom);
         c *= std::polar(s, -2.0 * M_PI * (double)((int64_t)r * k % N) / N);
-        row[((4 * k3 + r / 2) * 256 + t) * 2 + (r & 1)] = make_float2((float)c.real(), (float)c.imag());
+        row[(((zoom / 2) * k3 + r / 2) * 256 + t) * 2 + (r & 1)] = make_float2((float)c.real(), (float)c.imag());
       }
     }
   }
@@ -513,15 +515,18 @@ bool pc_edge_map_k(int K, int side, int lmod, PcEdge &out) {
 //   5: zoom 4 FIR taps g0 | g1 (74 floats); 12 / 13: zoom-4 left / right map for L mod 4 = arg
 //   built now; 14: the shipped zoom-4 map arg; 6: zoom 2 FIR taps M + its input-rate and
 //   output-rate sections' a1, a2 (41 floats); 15 / 16: zoom-2 left / right map for L mod 2 = arg
-//   built now; 17: the shipped zoom-2 map arg; 18: the FC twiddles W_1024^k (2048 floats);
-//   19: the FC filter row for f_lo / fs = arg / 2^20 (kFcRow complex as floats, kernel order).
+//   built now; 17: the shipped zoom-2 map arg; 18 / 20: the FC twiddles W_M^k of zoom 8 / 4
+//   (M = 1024 / 2048, as floats); 19 / 21: the FC filter row of zoom 8 / 4 for f_lo / fs =
+//   arg / 2^20 (kFcRow complex as floats, kernel order).
 extern "C" int zfft__pc_tables(int what, int arg, float *out, int cap) {
   using namespace zfft;
-  if (what == 18 || what == 19) {
-    const int n = what == 18 ? 2 * (kFcN / 8) : 2 * kFcRow;
+  if (what >= 18 && what <= 21) {
+    const int zoom = what <= 19 ? 8 : 4;
+    const bool tw = what == 18 || what == 20;
+    const int n = tw ? 2 * (kFcN / zoom) : 2 * kFcRow;
     if (cap < n) return -2;
-    if (what == 18) fc_build_twiddles((float2 *)out);
-    else if (!fc_build_row((double)arg / (double)(1 << 20), (float2 *)out)) return -1;
+    if (tw) fc_build_twiddles(kFcN / zoom, (float2 *)out);
+    else if (!fc_build_row(zoom, (double)arg / (double)(1 << 20), (float2 *)out)) return -1;
     return n;
   }
   if (what == 0 || what == 1) {

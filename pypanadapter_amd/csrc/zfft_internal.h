@@ -276,12 +276,18 @@ hipError_t launch_pc_edge(const InDesc &in, const float2 *lo, float2 *out, int64
 constexpr int kFcN = 8192, kFcStep = FC_STEP;
 constexpr int kFcK = (kFcN - 512 * kFcStep) / 2;   // 768
 constexpr int kFcP = 64 * kFcStep;                 // 832
-constexpr int kFcRow = kFcN;                       // C[k][r] per LO row, [4 k3 + r/2][t] (r, r+1) pairs
-// C for LO frequency ratio f_lo / fs into row (kFcRow entries); false if the model is unavailable
-bool fc_build_row(double lo_ratio, float2 *row);
-void fc_build_twiddles(float2 *tw);                // W_1024^k, k < 1024
+// Zoom 4 (cfg1): four residues of 2048 points, the zoom-4 model truncated at |k| <= 512 (tail
+// 1.4e-8 of sum |g|), windows advancing 7168 samples (1792 outputs).
+constexpr int kFc4Step = 14;
+constexpr int kFc4K = (kFcN - 512 * kFc4Step) / 2;  // 512
+constexpr int kFc4P = 512 * kFc4Step / 4;          // 1792
+constexpr int kFcRow = kFcN;  // C[k][r] per LO row, v4f pairs [(zoom / 2) k3 + r / 2][t] (r, r+1)
+// C for zoom 8 or 4 and LO frequency ratio f_lo / fs into row (kFcRow entries); false if the
+// model is unavailable
+bool fc_build_row(int zoom, double lo_ratio, float2 *row);
+void fc_build_twiddles(int M, float2 *tw);         // W_M^k, k < M (M = kFcN / zoom)
 hipError_t launch_fc_decim(const InDesc &in, const float2 *lo, const float2 *tab, int64_t row_stride,
-                           float2 *out, int64_t n3, int frames, hipStream_t st);
+                           float2 *out, int64_t nd, int frames, int zoom, hipStream_t st);
 
 struct WelchGeom {
   int n_fft, log2n;

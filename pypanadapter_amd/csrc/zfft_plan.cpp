@@ -815,6 +815,10 @@ constexpr int kPc4WalkMinFrames = 512;
 // 0.107, 512: 0.75 / 0.74 / 0.52, 4096: - / 4.69 / 3.44; 2^20-sample frames 1: 0.057 / 1.23 /
 // 0.066, 64: 0.37 / 1.30 / 0.26, 2048: - / 9.05 / 6.61.
 constexpr int kFcMinFrames = 16;
+// Zoom 4 (cfg1's 262,144-sample frames, ms per call, tiles / walk / FC, profiles/r06fc/r06fc8):
+// 1: 0.055 / 0.39 / 0.062, 16: 0.080 / 0.41 / 0.083, 64: 0.146 / 0.43 / 0.129, 512: 0.93 / 0.80 /
+// 0.61, 4096: - / 5.06 / 3.77.
+constexpr int kFc4MinFrames = 32;
 // FC takes frames of >= kFcN samples below 2^31 bytes (its buffer loads' 32-bit offsets).
 bool fc_fits(const zfft_plan *p, int64_t L) {
   return L >= kFcN && L * (int64_t)in_elem_bytes(p->cfg.in_dtype) < ((int64_t)1 << 31);
@@ -904,6 +908,8 @@ int ensure_pc(zfft_plan *p) {
   return ZFFT_OK;
 }
 
+// FC's zoom on this plan: 4 at zoom 4, else 8 (zoom 8 and the head of zoom >= 16)
+int fc_zoom(const zfft_plan *p) { return p->K == 2 ? 4 : 8; }
 // FC tables for the plan's LO rows (host fp64 build, fc_build_row; one synchronous upload when
 // the LO frequencies change, after the plan's enqueued work)
 int ensure_fc(zfft_plan *p) {
@@ -913,15 +919,16 @@ int ensure_fc(zfft_plan *p) {
   if (p->fc_tab.p && p->fc_built == ratios) return ZFFT_OK;
   int rc = quiesce(p);
   if (rc) return rc;
+  const int zoom = fc_zoom(p), M = kFcN / zoom;
   std::vector<float2> h;
   try {
-    h.resize(kFcN / 8 + ratios.size() * (size_t)kFcRow);
+    h.resize(M + ratios.size() * (size_t)kFcRow);
   } catch (const std::bad_alloc &) {
     return fail(ZFFT_ENOMEM, "FC table host staging allocation failed");
   }
-  fc_build_twiddles(h.data());
+  fc_build_twiddles(M, h.data());
   for (size_t k = 0; k < ratios.size(); ++k)
-    if (!fc_build_row(ratios[k], h.data() + kFcN / 8 + k * kFcRow))
+    if (!fc_build_row(zoom, ratios[k], h.data() + M + k * kFcRow))
       return fail(ZFFT_EINTERNAL, "FC table: model response unavailable");
   hipError_t e = p->fc_tab.ensure(h.size() * sizeof(float2));
   if (e != hipSuccess) return fail(ZFFT_ENOMEM, "FC table allocation failed");
@@ -939,7 +946,7 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
            bool walk, const float2 **out, hipStream_t st, int K, bool fc = false) {
   int rc = ensure_pc(p);
   if (rc) return rc;
-  fc = fc && walk && K == kPcStages;
+  fc = fc && walk && (K == kPcStages || K == 2);
   if (fc && (rc = ensure_fc(p))) return rc;
   const int64_t n3 = n[K];
   const PcTab *tab = p->pc_tab.as<PcTab>();
@@ -969,7 +976,8 @@ int run_pc(zfft_plan *p, const InDesc &in, int64_t L, int frames, const std::vec
     e = hipEventRecord(p->fork_ev, st);
     if (e == hipSuccess) e = hipStreamWaitEvent(p->side_st, p->fork_ev, 0);
     if (e != hipSuccess) return hip_fail(e, "side stream fork");
-    if (fc) e = launch_fc_decim(in, p->lo.as<float2>(), p->fc_tab.as<float2>(), kFcRow, p->pong.as<float2>(), n3, frames, st);
+    if (fc) e = launch_fc_decim(in, p->lo.as<float2>(), p->fc_tab.as<float2>(), kFcRow, p->pong.as<float2>(), n3, frames,
+                                K == 2 ? 4 : 8, st);
     else if (K == 2) e = launch_pc_walk4(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, p->pc_tab4.as<PcTab4>(), st);
     else e = launch_pc_walk(in, p->lo.as<float2>(), p->pong.as<float2>(), n3, frames, tab, st);
     if (e != hipSuccess) return hip_fail(e, fc ? "fc_decim launch" : "pc_walk launch");
@@ -1102,9 +1110,11 @@ int run_decimator(zfft_plan *p, const InDesc &in, int64_t L, int frames,
   if (pc2 && (p->path >= 4 || (p->path == 0 && (frames < kPc2TilesMaxFrames || !xa_auto))))
     return run_pc(p, in, L, frames, n, false, out, st, 1);
   // zoom 4: the tiles below 512 frames per call, the walk from there (both on request too)
-  if (pc4 && (p->path >= 4 || p->path == 0))
-    return run_pc(p, in, L, frames, n, p->path >= 5 || (p->path == 0 && frames >= kPc4WalkMinFrames), out,
-                  st, p->K);
+  if (pc4 && (p->path >= 4 || p->path == 0)) {
+    const bool fc4 = fc_fits(p, L) && (p->path == 6 || (p->path == 0 && frames >= kFc4MinFrames));
+    return run_pc(p, in, L, frames, n, fc4 || p->path >= 5 || (p->path == 0 && frames >= kPc4WalkMinFrames),
+                  out, st, p->K, fc4);
+  }
   const bool walk = p->path >= 5 || (p->path == 0 && frames >= kPcWalkMinFrames);
   // FC in the walk's place: on request (6) and automatic from kFcMinFrames frames per call
   const bool fc = fc_fits(p, L) && (p->path == 6 || (p->path == 0 && frames >= kFcMinFrames));

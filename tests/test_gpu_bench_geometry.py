@@ -44,7 +44,7 @@ def test_bench_batch_rows_vs_oracle(oracle_lib, torch_dev, config, in_dtype):
         names = plan.launch_names()
     assert names[0] in ("xa_stage_mix", "pc_fir", "pc_walk", "pc_walk4", "fc_decim"), names  # the schedule the bench times
     if config == "cfg1":
-        assert names[0] == "pc_walk4", names  # zoom 4 at F = 4096: the walk (round 6, r06k)
+        assert names[0] == "fc_decim", names  # zoom 4 at F = 4096: FC (round 6, r06fc8)
     if config in ("cfg2", "cfg3", "cfg5"):
         assert names[0] == "fc_decim", names  # zoom 8 from 16 frames per call: FC (round 6, r06fc3)
     host = rows.cpu().numpy()

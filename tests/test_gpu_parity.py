@@ -487,10 +487,11 @@ def test_facade_matches_reference_rows():
                                         (8, 16, 299008, "fc"), (8, 384, 299008, "fc"),
                                         (8, 768, 1048576, "fc"), (8, 1024, 32768, "fc"),
                                         (8, 1023, 32768, "fc"), (8, 4, 8192, "exact"),
-                                        (4, 1, 262144, "pc"), (4, 256, 262144, "pc"),
-                                        (4, 384, 262144, "pc"), (4, 64, 1048576, "pc"),
-                                        (4, 511, 65536, "pc"), (4, 512, 65536, "walk4"),
-                                        (4, 1024, 65536, "walk4"), (4, 768, 8192, "xa"),
+                                        (4, 1, 262144, "pc"), (4, 31, 262144, "pc"),
+                                        (4, 32, 262144, "fc"), (4, 256, 262144, "fc"),
+                                        (4, 384, 262144, "fc"), (4, 64, 1048576, "fc"),
+                                        (4, 511, 65536, "fc"), (4, 512, 65536, "fc"),
+                                        (4, 1024, 65536, "fc"), (4, 768, 8192, "xa"),
                                         (2, 512, 65536, "xa"), (2, 511, 65536, "pc2"), (2, 8, 262144, "pc2"),
                                         (2, 600, 1048576, "pc2"), (2, 768, 1048576, "xa"),
                                         (2, 8, 8192, "exact"),
@@ -592,15 +593,15 @@ def test_xa_refuses_frames_beyond_32bit_offsets():
                                 torch.cuda.current_stream().cuda_stream)
 
 
-@pytest.mark.parametrize("z,F,L,first,waits", [(8, 1024, 32768, "fc_decim", 1), (4, 2100, 32768, "pc_walk4", 1),
+@pytest.mark.parametrize("z,F,L,first,waits", [(8, 1024, 32768, "fc_decim", 1), (4, 2100, 32768, "fc_decim", 1),
                                                 (2, 2100, 32768, "xa_stage_mix", 1), (2, 500, 32768, "pc_tail", 1),
-                                                (4, 500, 32768, "pc_fir", 1)])
+                                                (4, 500, 32768, "fc_decim", 1), (4, 20, 32768, "pc_fir", 0)])
 def test_batched_host_call_times_every_batch_with_one_schedule(z, F, L, first, waits):
     """zfft_process splits a >= 64 MB call into batches (H2D of k+1 under compute of k): the
     timings cover every batch, and a call the XA tiles would take keeps them in every batch
     (batches of >= 384 frames for these lengths, or a single batch) instead of splitting into
-    batches too small for them; PC (zoom 8 and 4: the tiles below the walk's batch, the walk
-    from it) takes any batch by its own frame count."""
+    batches too small for them; zoom 8 and 4 (PC's tiles below FC's batch, FC from it) take any
+    batch by its own frame count."""
     from pypanadapter_amd import ZoomFFT
     x = np.zeros((F, L), np.complex64)
     x[:, ::3] = 1.0

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Same-box A/B of the zoom-8 decimators: per-call device time (HIP events, median of 5 after 2
+"""Same-box A/B of the zoom-8 and zoom-4 decimators: per-call device time (HIP events, median of 5 after 2
 warm calls) of the PC tiles (path 4, small batches), the walk (path 5) and FC (path 6) at cfg2's
 and cfg5's frame lengths over batch sizes, and of zoom 16 (PC head + tail, walk vs FC head);
 paths alternate per size; per-launch times of the largest batch.  Stamped with the kernel-source
@@ -15,6 +15,7 @@ CASES = {  # name: (n_fft, zoom, L, {paths: frame counts})
     "cfg2_L299008": (4096, 8, 299008, {(4, 5, 6): [1, 16, 64, 256, 512, 1024], (5, 6): [2048, 4096]}),
     "cfg5_L1048576": (65536, 8, 1048576, {(4, 5, 6): [1, 64, 512, 1024], (5, 6): [2048]}),
     "z16_L299008": (4096, 16, 299008, {(5, 6): [1, 64, 512, 4096]}),
+    "cfg1_z4_L262144": (1024, 4, 262144, {(4, 5, 6): [1, 16, 64, 256, 512, 1024], (5, 6): [2048, 4096]}),
 }
 
 
