@@ -28,7 +28,7 @@ from pypanadapter_amd import build  # noqa: E402
 
 
 def kname(name: str) -> str:
-    m = re.search(r"zfft::(?:xa::|pc::)?([a-z_0-9]+)(<[^>(]*>)?", name)
+    m = re.search(r"zfft::(?:xa::|pc::|fc::)?([a-z_0-9]+)(<[^>(]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name[:60]
 
 

@@ -35,7 +35,7 @@ XCDS = 8
 
 
 def kname(name):
-    m = re.search(r"zfft::(?:xa::|pc::)?([a-z_0-9]+)(<[^>(]*>)?", name)
+    m = re.search(r"zfft::(?:xa::|pc::|fc::)?([a-z_0-9]+)(<[^>(]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else None
 
 
