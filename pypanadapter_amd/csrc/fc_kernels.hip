@@ -41,6 +41,9 @@
 #ifndef FC_KO
 #define FC_KO 0
 #endif
+#ifndef FC_HOLD
+#define FC_HOLD (-1)  // diagnostic override of fc_hold for every non-cu8 instantiation
+#endif
 
 
 namespace zfft {
@@ -155,6 +158,12 @@ __device__ __forceinline__ typename RawP<DT>::T load_pair_b(__amdgpu_buffer_rsrc
   else if constexpr (DT == kInCU8) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, aux));
   else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, aux));
 }
+// How many of a thread's 16 C pairs stay in registers for the whole kernel instead of being
+// re-read from L2 every block: as many as each instantiation holds without spilling at 2 WG/CU
+// (cu8 has no room; zoom-8 complex64 8: fc_decim 2.62 -> 2.55 ms at cfg2, r06fc10)
+constexpr int fc_hold(int Z, int DT) {
+  return DT == kInCU8 ? 0 : DT == kInC64 ? (Z == 8 ? 8 : 4) : 12;
+}
 
 // One workgroup walks blocks [bpc * blockIdx.x, +bpc) of frame blockIdx.y.  tab: W_M^k (k < M),
 // then per LO row (row_stride apart) C as v4f pairs [(Z / 2) k3 + r / 2][t] (r, r + 1) for thread t
@@ -198,6 +207,12 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
   }
   // pass C: k1 = t >> 4, k2 = t & 15 -> kp = k1 + 16 k2
   const int kp = (t >> 4) + 16 * (t & 15);
+  // the first HOLD of its 16 C pairs held for the whole kernel (the rest read per block)
+  constexpr int HOLD = FC_HOLD >= 0 ? (DT == kInCU8 ? 0 : FC_HOLD) : fc_hold(Z, DT);
+  v4f ch[HOLD > 0 ? HOLD : 1];
+#pragma unroll
+  for (int i = 0; i < HOLD; ++i)
+    ch[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(crs, (uint32_t)(16 * t), 4096 * i, 0));
   // inverse twiddle bases, conjugated: stage 1 W_M^kp, 2 W_256^(t & 63), 3 W_64^(t & 15),
   // 4 W_16^(t & 3) (the digits below each stage's)
   const v2f ib0 = conj(tw[kp]), ib1 = conj(tw[(M / 256) * (t & 63)]), ib2 = conj(tw[(M / 64) * (t & 15)]),
@@ -313,6 +328,7 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         cr[i] = (FC_KO & 2) ? v4f{1.f, 0.5f, 0.25f, 1.f}
+                : i < HOLD  ? ch[i < HOLD ? i : 0]
                             : __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(crs, (uint32_t)(16 * t), 4096 * i, 0));
       // one residue pair at a time: its R1 values, DFT each, accumulated into Yf (the whole
       // window's 32 values and C's 32 at once spilled)
