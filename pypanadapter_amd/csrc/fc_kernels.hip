@@ -41,6 +41,9 @@
 #ifndef FC_KO
 #define FC_KO 0
 #endif
+#ifndef FC_WSYNC
+#define FC_WSYNC 1  // A/B knob: 0 = a workgroup barrier between the wave-local inverse stages
+#endif
 #ifndef FC_HOLD
 #define FC_HOLD (-1)  // diagnostic override of fc_hold for every non-cu8 instantiation
 #endif
@@ -158,6 +161,19 @@ __device__ __forceinline__ typename RawP<DT>::T load_pair_b(__amdgpu_buffer_rsrc
   else if constexpr (DT == kInCU8) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, aux));
   else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, aux));
 }
+// Between two inverse stages whose LDS slots stay inside one wave: a wave's LDS operations
+// complete in issue order, so ordering the compiler's view (wavefront-scope fences around a
+// wave barrier) is all it takes -- no s_barrier
+__device__ __forceinline__ void stage_sync() {
+  if (FC_WSYNC) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
 // How many of a thread's 16 C pairs stay in registers for the whole kernel instead of being
 // re-read from L2 every block: as many as each instantiation holds without spilling at 2 WG/CU
 // (cu8 has no room; zoom-8 complex64 8: fc_decim 2.62 -> 2.55 ms at cfg2, r06fc10)
@@ -372,12 +388,14 @@ __global__ void __launch_bounds__(256, 2) fc_decim_kernel(InDesc in, const v2f *
         for (int a = 0; a < 4; ++a) sl[a0 + 1088 * h + st * a] = v[a];
       }
     };
+    // stages 2..4 read and write only the slots of their wave's b0 (t >> 6, + 4 h): the
+    // exchanges between them are wave-local, stage 5 reads every wave's
     istage(a2, 68, ib1);
-    __syncthreads();
+    stage_sync();
     istage(a3, 17, ib2);
-    __syncthreads();
+    stage_sync();
     istage(a4, 4, ib3);
-    __syncthreads();
+    __syncthreads();  // (stage 5 inside the wave, outputs R1 apart: 3.11 -> 3.31 ms, r06fc12)
     // stage 5: radix 4 over a0 -> b4; outputs j = u + (M / 4) b4
     {
       v2f *o = out + f * nd + m0;

@@ -174,3 +174,28 @@ def test_fc_block_in_the_kernels_index_maps(Z):
     jv = np.arange(K // Z, K // Z + P)
     err = np.abs(y[jv] - direct[jv]).max() / np.abs(direct[jv]).max()
     assert err < 1e-6, err               # the row's fp32 rounding
+
+
+@pytest.mark.parametrize("Z", [8, 4])
+def test_fc_inverse_stages_2_to_4_are_wave_local(Z):
+    """fc_kernels.hip drops the workgroup barriers between inverse stages 2, 3 and 4 (stage_sync):
+    every slot a wave's butterflies read or write there has b0 = i >> 8 equal to (t >> 6) + 4 h,
+    and each stage's slots of one wave are the same set -- no slot crosses waves until stage 5."""
+    M = N // Z
+    NB = M // 1024
+    bases = ((lambda u: (u & 63) + 256 * (u >> 6), 64),
+             (lambda u: (u & 15) + 64 * ((u >> 4) & 3) + 256 * (u >> 6), 16),
+             (lambda u: (u & 3) + 16 * ((u >> 2) & 3) + 64 * ((u >> 4) & 3) + 256 * (u >> 6), 4))
+    for w in range(4):
+        sets = []
+        for base, S in bases:
+            slots = set()
+            for t in range(64 * w, 64 * w + 64):
+                for h in range(NB):
+                    for a in range(4):
+                        i = base(t) + 1024 * h + S * a        # ps(i) + 1088 h = ps(i + 1024 h)
+                        assert i >> 8 == (t >> 6) + 4 * h
+                        slots.add(i)
+            sets.append(slots)
+        assert sets[0] == sets[1] == sets[2]
+        assert len(sets[0]) == 256 * NB
