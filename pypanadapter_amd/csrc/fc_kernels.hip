@@ -176,9 +176,10 @@ __device__ __forceinline__ void stage_sync() {
 
 // How many of a thread's 16 C pairs stay in registers for the whole kernel instead of being
 // re-read from L2 every block: as many as each instantiation holds without spilling at 2 WG/CU
-// (cu8 has no room; zoom-8 complex64 8: fc_decim 2.62 -> 2.55 ms at cfg2, r06fc10)
+// (cu8 has no room; against none, complex64 8 at zoom 8: fc_decim 2.62 -> 2.55 ms at cfg2,
+// r06fc10; 6 at zoom 4 and 14 for complex32 beat 4 and 12 by 1.1 / 0.6 % per step, r06fc13)
 constexpr int fc_hold(int Z, int DT) {
-  return DT == kInCU8 ? 0 : DT == kInC64 ? (Z == 8 ? 8 : 4) : 12;
+  return DT == kInCU8 ? 0 : DT == kInC64 ? (Z == 8 ? 8 : 6) : 14;
 }
 
 // One workgroup walks blocks [bpc * blockIdx.x, +bpc) of frame blockIdx.y.  tab: W_M^k (k < M),
