@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from conftest import assert_row_close, case_input, check_rel, golden_cases, golden_rows
-from test_gpu_pc import PC_LENGTHS, _encode, _frames
+from test_gpu_pc import PC_LENGTHS, PC_TOL, _encode, _frames
 
 pytestmark = pytest.mark.gpu
 # measured worst 5.96e-7 at K = 768 (tolerance ledger, keys fc8/ fc4/..., profiles/r06fc/r06fc8) + ~20 %
@@ -45,6 +45,30 @@ def test_fc_decimate_vs_oracle(oracle_lib, flip):
         ref = oracle_lib.zoomfft(x[::-1].copy() if flip else x, 8, 2.4e6)
         assert d.shape == ref.shape, (L, d.shape, ref.shape)
         check_rel(d, ref, FC_TOL, "fc8/decimate", (L, flip))
+
+
+@pytest.mark.parametrize("L,kernel", [((1 << 28) - 3, "fc_decim"), ((1 << 28) + 5, "pc_walk")],
+                         ids=["fc_largest_frame", "walk_past_2GiB"])
+def test_fc_largest_frames_ends_vs_oracle(oracle_lib, L, kernel):
+    """FC addresses a frame through 32-bit buffer offsets (launch_fc_decim, fc_fits): the largest
+    complex64 frame it takes (< 2^31 bytes) runs FC, one past it runs the walk even with path 6
+    forced.  Size-independent check at 2 GiB, both flips: the first and last 98,304 decimated
+    samples equal the oracle's on a 2^20-sample prefix and on an 8-aligned suffix of the frame
+    (the cascade has forgotten the far end long before; f_lo = 0 keeps the mix shift-invariant)."""
+    from pypanadapter_amd import ZoomFFT
+    x = np.random.default_rng(4490).standard_normal(2 * L, dtype=np.float32).view(np.complex64)
+    L2, m = (1 << 20) + L % 8, 98304
+    tol = FC_TOL if kernel == "fc_decim" else PC_TOL
+    for flip in (False, True):
+        s = x[::-1] if flip else x
+        with ZoomFFT(4096, 8, 2.4e6, f_lo=0.0, flip=flip) as plan:
+            plan.set_path(6)
+            d, names = _decimate_named(plan, x)
+        assert kernel in names and ("fc_decim" in names) == (kernel == "fc_decim"), names
+        head = oracle_lib.zoomfft(np.ascontiguousarray(s[:L2]), 8, 2.4e6, f_lo=0.0)
+        tail = oracle_lib.zoomfft(np.ascontiguousarray(s[L - L2:]), 8, 2.4e6, f_lo=0.0)
+        check_rel(d[:m], head[:m], tol, f"{kernel}/largest_frame", ("head", flip))
+        check_rel(d[-m:], tail[-m:], tol, f"{kernel}/largest_frame", ("tail", flip))
 
 
 def test_fc_lo_offsets_vs_oracle(oracle_lib):
