@@ -13,8 +13,10 @@ from conftest import assert_row_close, case_input, check_rel, golden_cases, gold
 from test_gpu_pc import PC_LENGTHS, PC_TOL, _encode, _frames
 
 pytestmark = pytest.mark.gpu
-# measured worst 5.96e-7 at K = 768 (tolerance ledger, keys fc8/ fc4/..., profiles/r06fc/r06fc8) + ~20 %
-FC_TOL = 7.2e-7
+# the bound include/zfft.h documents for path 6: measured worst 6.07e-7 at K = 768 (the 2 GiB frame,
+# fc_decim/largest_frame; 5.96e-7 fc8/decimate_lo; tolerance ledger profiles/r06tol/tol_ledger.json)
+# + 7 %; FC sums in a fixed order (no atomics), so the worst is the same on every run
+FC_TOL = 6.5e-7
 
 
 @pytest.fixture(scope="module", autouse=True)
